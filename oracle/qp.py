@@ -1,0 +1,239 @@
+"""numpy restatement of the per-step QP and its solution (ORACLE, tests only).
+
+The reference solves, every control step, the strictly convex QP built in
+``lib/mpc.py:318-335`` (MPCStateFB.step) / ``lib/mpc.py:461-478`` (MPCOutputFB.step)
+with cvxpy.  cvxpy (and its default backend) is absent in this image and
+unpinned upstream, so the QP arithmetic cannot be run from the reference; see
+``oracle/__init__.py`` for how parity is anchored instead.
+
+This module provides
+  * ``ipm``        -- the dense Mehrotra predictor-corrector IPM specified in
+                      DESIGN.md §3 (the algorithm the HIP kernel implements),
+                      vectorised numpy, one instance at a time;
+  * ``certify``    -- an independent active-set KKT polish + certificate: returns
+                      the exact optimum (to ~1e-13) and the KKT residuals, so a
+                      solution is judged against the *unique* optimum, not
+                      against another IPM;
+  * ``lp_margin``  -- the HiGHS LP max-slack margin t* = max{t : G u + t <= w,
+                      lb <= u <= ub}; t* >= 0 <=> feasible.  Ground truth for the
+                      optimal / primal-infeasible status (mpc.py:336-338).
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.optimize import linprog
+
+STATUS_OPTIMAL, STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL = 0, 1, 2, 3
+STATUS_NAMES = {0: "optimal", 1: "primal_infeasible", 2: "max_iter", 3: "numerical"}
+
+# Settings shared with oracle/ipm.c and carmpc_amd/csrc
+TOL_RES = 1e-10
+TOL_MU = 1e-12
+MAX_ITER = 60
+STEP_FRAC = 0.99
+UNBOXED_BOUND = 1e9        # |u_i| bound assumed by the Farkas test for unboxed variables
+PRE_TOL = 1e-9             # zero-row precondition tolerance
+ZERO_ROW = 1e-12           # rows with ||G_r||_2 <= ZERO_ROW * max_r ||G_r||_2 are x0-only rows
+
+
+def normalize_rows(G, w0, E):
+    """Split general rows into QP rows (unit 2-norm) and x0-only rows (G_r == 0).
+    Returns (Gn, w0n, En, keep_mask, pre_w0, pre_E)."""
+    nrm = np.linalg.norm(G, axis=1) if G.size else np.zeros(len(w0))
+    thr = ZERO_ROW * (nrm.max() if nrm.size else 0.0)
+    keep = nrm > thr
+    inv = 1.0 / nrm[keep]
+    return (G[keep] * inv[:, None], w0[keep] * inv, E[keep] * inv[:, None], keep,
+            w0[~keep], E[~keep])
+
+
+def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
+        trace=None):
+    """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
+
+    G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
+    Returns (u, status, iterations, z_g)."""
+    n = len(q)
+    p = G.shape[0]
+    boxed = lb is not None
+    if boxed:
+        lb = np.asarray(lb, float); ub = np.asarray(ub, float)
+        blo, bhi = lb, ub
+        u = np.clip(np.zeros(n), lb, ub)
+    else:
+        blo = np.full(n, -UNBOXED_BOUND); bhi = np.full(n, UNBOXED_BOUND)
+        u = np.zeros(n)
+    nb = n if boxed else 0
+    m = p + 2 * nb
+    s = np.maximum(w - G @ u, 1.0); z = np.ones(p)
+    if boxed:
+        su = np.maximum(ub - u, 1.0); sl = np.maximum(u - lb, 1.0)
+    else:
+        su = np.ones(0); sl = np.ones(0)
+    zu = np.ones(nb); zl = np.ones(nb)
+    bnorm = 1.0 + max(np.abs(w).max() if p else 0.0,
+                      np.abs(ub).max() if boxed else 0.0, np.abs(lb).max() if boxed else 0.0)
+    qnorm = 1.0 + (np.abs(q).max() if n else 0.0)
+    bound_abs = np.maximum(np.abs(blo), np.abs(bhi))
+
+    def box_T(vu, vl):  # contribution of box rows to A'v
+        return (vu - vl) if boxed else 0.0
+
+    for it in range(max_iter):
+        Gu = G @ u
+        rp = Gu + s - w
+        rpu = (u + su - ub) if boxed else su
+        rpl = (-u + sl + lb) if boxed else sl
+        rd = H @ u + q + G.T @ z + box_T(zu, zl)
+        mu = (s @ z + su @ zu + sl @ zl) / max(m, 1)
+        rpn = max(np.abs(rp).max() if p else 0.0, np.abs(rpu).max() if nb else 0.0,
+                  np.abs(rpl).max() if nb else 0.0)
+        rdn = np.abs(rd).max()
+        if trace is not None:
+            trace.append((it, mu, rpn, rdn))
+        if not np.isfinite(mu) or not np.isfinite(rdn):
+            return u, STATUS_NUMERICAL, it, z
+        if rpn <= tol * bnorm and rdn <= tol * qnorm and mu <= tol_mu:
+            return u, STATUS_OPTIMAL, it, z
+        # Farkas test: for every u in the box, (G'z)'u >= lo; if lo > w'z then no u
+        # satisfies G u <= w (z >= 0).  Rigorous when all variables are boxed.
+        if p:
+            c = G.T @ z
+            lo = np.minimum(c * blo, c * bhi).sum()
+            wz = w @ z
+            if lo - wz > 1e-12 * (np.abs(c) @ bound_abs + np.abs(w) @ z):
+                return u, STATUS_INFEASIBLE, it, z
+        d = z / s
+        M = H + (G.T * d) @ G
+        if boxed:
+            M[np.diag_indices(n)] += zu / su + zl / sl
+        Lc = _chol_guarded(M)
+
+        def solve(rc, rcu, rcl):
+            t = (rc - z * rp) / s
+            rhs = -rd + G.T @ t
+            if boxed:
+                rhs = rhs + (rcu - zu * rpu) / su - (rcl - zl * rpl) / sl
+            du = _chol_solve(Lc, rhs)
+            ds = -rp - G @ du
+            dz = (-rc - z * ds) / s
+            if boxed:
+                dsu = -rpu - du; dsl = -rpl + du
+                dzu = (-rcu - zu * dsu) / su; dzl = (-rcl - zl * dsl) / sl
+            else:
+                dsu = dsl = dzu = dzl = np.zeros(0)
+            return du, ds, dz, dsu, dzu, dsl, dzl
+
+        du, ds, dz, dsu, dzu, dsl, dzl = solve(s * z, su * zu, sl * zl)
+        a_aff = min(1.0, _maxstep(s, ds), _maxstep(z, dz), _maxstep(su, dsu),
+                    _maxstep(zu, dzu), _maxstep(sl, dsl), _maxstep(zl, dzl))
+        mu_aff = ((s + a_aff * ds) @ (z + a_aff * dz) + (su + a_aff * dsu) @ (zu + a_aff * dzu)
+                  + (sl + a_aff * dsl) @ (zl + a_aff * dzl)) / max(m, 1)
+        sigma = (mu_aff / mu) ** 3
+        smu = sigma * mu
+        du, ds, dz, dsu, dzu, dsl, dzl = solve(s * z + ds * dz - smu, su * zu + dsu * dzu - smu,
+                                               sl * zl + dsl * dzl - smu)
+        a = min(1.0, STEP_FRAC * min(_maxstep(s, ds), _maxstep(z, dz), _maxstep(su, dsu),
+                                     _maxstep(zu, dzu), _maxstep(sl, dsl), _maxstep(zl, dzl)))
+        u = u + a * du; s = s + a * ds; z = z + a * dz
+        su = su + a * dsu; zu = zu + a * dzu; sl = sl + a * dsl; zl = zl + a * dzl
+    return u, STATUS_MAXITER, max_iter, z
+
+
+def _maxstep(v, dv):
+    neg = dv < 0
+    if not neg.any():
+        return np.inf
+    return float(np.min(-v[neg] / dv[neg]))
+
+
+def _chol_guarded(M):
+    """Right-looking Cholesky; a non-positive pivot is replaced by 1e128 (its
+    direction is frozen) -- the same guard as oracle/ipm.c and the HIP kernel."""
+    n = M.shape[0]
+    L = np.array(M, dtype=float)
+    for k in range(n):
+        piv = L[k, k]
+        if not piv > 0:
+            piv = 1e128
+        lkk = np.sqrt(piv)
+        L[k, k] = lkk
+        L[k + 1:, k] /= lkk
+        L[k + 1:, k + 1:] -= np.outer(L[k + 1:, k], L[k + 1:, k])
+    return np.tril(L)
+
+
+def _chol_solve(L, b):
+    from scipy.linalg import solve_triangular
+    y = solve_triangular(L, b, lower=True)
+    return solve_triangular(L.T, y, lower=False)
+
+
+def certify(H, q, G, w, lb, ub, u_hint, act_tol=1e-7):
+    """Active-set KKT polish + certificate.
+
+    Takes the active set suggested by ``u_hint`` (rows with slack <= act_tol*(1+|b|)),
+    solves the equality-constrained KKT system exactly, and reports
+    (u_exact, certified, residuals) with residuals = (max primal violation,
+    min multiplier, max stationarity residual).  certified <=> violation <= 1e-9,
+    multipliers >= -1e-9, stationarity <= 1e-9 * (1 + |q|)."""
+    n = len(q)
+    rows = [G]; rhs = [w]
+    if lb is not None:
+        rows += [np.eye(n), -np.eye(n)]; rhs += [ub, -lb]
+    A = np.vstack(rows); b = np.hstack(rhs)
+    best = None
+    for tol in (act_tol, 1e-9, 1e-6, 1e-5):
+        slack = b - A @ u_hint
+        act = np.where(slack <= tol * (1 + np.abs(b)))[0]
+        Aa = A[act]; k = len(act)
+        KKT = np.block([[H, Aa.T], [Aa, np.zeros((k, k))]])
+        sol = np.linalg.lstsq(KKT, np.hstack([-q, b[act]]), rcond=None)[0]
+        ue, lam = sol[:n], sol[n:]
+        viol = float(max((A @ ue - b).max(), 0.0)) if len(b) else 0.0
+        lmin = float(lam.min()) if k else 0.0
+        stn = float(np.abs(H @ ue + q + Aa.T @ lam).max())
+        ok = viol <= 1e-9 and lmin >= -1e-9 and stn <= 1e-9 * (1 + np.abs(q).max())
+        if ok:
+            return ue, True, (viol, lmin, stn)
+        if best is None:
+            best = (ue, False, (viol, lmin, stn))
+    return best
+
+
+def lp_margin(G, w, lb, ub, cap=1.0):
+    """HiGHS: t* = max t s.t. G u + t 1 <= w, lb <= u <= ub, t <= cap.
+    Feasible iff t* >= 0 (G rows normalised => t* is a Euclidean slack)."""
+    n = G.shape[1]
+    c = np.zeros(n + 1); c[-1] = -1.0
+    A = np.hstack([G, np.ones((G.shape[0], 1))])
+    bounds = ([(l, h) for l, h in zip(lb, ub)] if lb is not None else [(None, None)] * n) + [(None, cap)]
+    r = linprog(c, A_ub=A, b_ub=w, bounds=bounds, method="highs")
+    if r.status != 0:
+        raise RuntimeError(f"HiGHS failed: {r.message}")
+    return float(r.x[-1])
+
+
+def solve_instance(asm, x0, xref=None, **kw):
+    """Full per-step oracle for one instance of an ``assembly.Assembly``:
+    preconditions on x0-only rows, normalised IPM, certificate.
+    Returns dict(status, iters, u, u_exact, certified, margin)."""
+    from .assembly import qp_data
+    q, w = qp_data(asm, x0, xref)
+    Gn, w0n, En, keep, pre_w0, pre_E = normalize_rows(asm.G, asm.w0, asm.E)
+    x0 = np.asarray(x0, float)
+    wn = w0n - En @ x0
+    pre = pre_w0 - pre_E @ x0
+    out = dict(q=q, w=wn)
+    if pre.size and pre.min() < -PRE_TOL:
+        out.update(status=STATUS_INFEASIBLE, iters=0, u=np.zeros(len(q)), u_exact=None,
+                   certified=False, margin=float(pre.min()))
+        return out
+    u, st, it, _ = ipm(asm.H, q, Gn, wn, asm.lb, asm.ub, **kw)
+    out.update(status=st, iters=it, u=u)
+    if st == STATUS_OPTIMAL:
+        ue, ok, res = certify(asm.H, q, Gn, wn, asm.lb, asm.ub, u)
+        out.update(u_exact=ue, certified=ok, kkt=res)
+    else:
+        out.update(u_exact=None, certified=False)
+    return out
