@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark: batched MPC QP solves/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[4], weak-scaled): every rank solves a shard of
+131,072 mixed Road*/Env instances (RoadEnv / RoadOneCarEnv / RoadMultipleCarsEnv,
+N=20, n=40, fp64), grouped by environment; at 8 GPUs that is the 1,048,576-instance
+config.  One timed step = one pass of the hot path (device QP solve of the whole
+shard, inputs resident in HBM).  The shard split needs no collective; the only
+communication is the max-over-ranks of the timing.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+ENVS = ("RoadEnv", "RoadOneCarEnv", "RoadMultipleCarsEnv")
+PER_GPU = 131072
+N_HOR = 20
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 dense (vector == matrix), spec
+HBM_PEAK_GBS = 8000.0
+
+
+def sample_shard(rank: int, B: int, goals):
+    """Config 5 inputs: env_id ~ U{0,1,2}, x in [g_x-25, g_x], y in [-3,3],
+    psi in [-pi/8, pi/8], v in [-1, 5]; grouped by env (sorted)."""
+    rng = np.random.default_rng(5 * 1000 + rank)
+    env = np.sort(rng.integers(0, len(ENVS), B))
+    gx = np.array([g[0] for g in goals])[env]
+    X = np.stack([gx - 25 * rng.random(B), rng.uniform(-3, 3, B), rng.uniform(-np.pi / 8, np.pi / 8, B),
+                  rng.uniform(-1, 5, B)], axis=1)
+    offsets = np.searchsorted(env, np.arange(len(ENVS) + 1))
+    return X, env, offsets
+
+
+def build_problems(device):
+    import contextlib
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE
+    from carmpc_amd.mpc import MPCStateFB
+    ctrls = []
+    with contextlib.redirect_stdout(sys.stderr):          # keep stdout to the one JSON line
+        for name in ENVS:
+            c = MPCStateFB(DT_CONTROL, N_HOR, LINEARIZE_STATE, LINEARIZE_INPUT, env=ENVIRONMENTS[name](),
+                           terminal_set_dir=os.path.join(REPO, "terminal_sets"), device=device)
+            c.qp  # assemble on the device now
+            ctrls.append(c)
+    return ctrls
+
+
+def cpu_baseline(ctrls, X, env, offsets, sample: int, threads: int):
+    """The oracle's C restatement of the same IPM (oracle/ipm.c, OpenMP), on a bounded sample."""
+    from oracle import assembly as oa
+    from oracle.cpu import CpuProblem
+    idx = np.concatenate([np.arange(offsets[j], min(offsets[j + 1], offsets[j] + sample // len(ENVS)))
+                          for j in range(len(ENVS))])
+    total_t, total_n, iters = 0.0, 0, {}
+    for j, name in enumerate(ENVS):
+        sel = idx[(idx >= offsets[j]) & (idx < offsets[j + 1])]
+        cp = CpuProblem(oa.build(name, N_HOR, terminal_set_dir=os.path.join(REPO, "terminal_sets")))
+        cp.solve(X[sel[:64]], threads=threads)                       # warm
+        t0 = time.perf_counter()
+        _, st, it = cp.solve(X[sel], threads=threads)
+        total_t += time.perf_counter() - t0
+        total_n += len(sel)
+        iters[name] = (float(it[st == 0].mean()) if (st == 0).any() else 0.0, float(it.mean()))
+    return total_n / total_t, total_n, iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--per-gpu", type=int, default=PER_GPU)
+    ap.add_argument("--cpu-sample", type=int, default=24576)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from carmpc_amd.qp import solve_segments
+    ctrls = build_problems(device)
+    probs = [c.qp for c in ctrls]
+    goals = [c.goal for c in ctrls]
+    X, env, offsets = sample_shard(rank, args.per_gpu, goals)
+    Xd = torch.as_tensor(X).to(device)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        u, st, it = solve_segments(probs, offsets, Xd, stream=stream)
+    torch.cuda.synchronize()
+
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev0[k].record(stream)
+        u, st, it = solve_segments(probs, offsets, Xd, stream=stream)
+        ev1[k].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev0, ev1)]))
+    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    # end-to-end (PCIe-inclusive) figure: H2D x0, solve, D2H u -- reported, never `value`
+    Xh = torch.as_tensor(X).pin_memory()
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    Xe = Xh.to(device, non_blocking=True)
+    ue, se, _ = solve_segments(probs, offsets, Xe, stream=stream)
+    uh = ue.to("cpu"); sh = se.to("cpu")
+    torch.cuda.synchronize()
+    e2e = args.per_gpu / (time.perf_counter() - te)
+
+    st_np = st.cpu().numpy(); it_np = it.cpu().numpy()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    total = args.per_gpu * world * args.steps
+    value = total / wall_max
+    status_split = {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
+                                                                      "numerical"))}
+    out = {
+        "metric": "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X",
+        "value": round(value, 1), "unit": "QP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded config-5 state distribution)",
+        "config": {"workload": "config5_mixed_road_envs_N20_weak", "per_gpu_batch": args.per_gpu,
+                   "global_batch": args.per_gpu * world, "envs": list(ENVS), "N": N_HOR, "n": 40,
+                   "p_qp_rows": [p.p for p in probs], "kernel": "ipm_dense (wavefront per QP, G/H in LDS)",
+                   "parallelism": f"shard{world} (no data-path collective)"},
+        "status_split": status_split,
+        "gpu_iters_mean": float(it_np[st_np == 0].mean()),
+        "e2e_qps_pcie_inclusive": round(e2e * world, 1),
+    }
+    # roofline: canonical FP64 flops with I_ref from the oracle on a sample of this batch
+    seg = np.diff(offsets)
+    if not args.no_cpu:
+        thr = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        cpu_qps, ncpu, iref = cpu_baseline(ctrls, X, env, offsets, args.cpu_sample, thr)
+        out["cpu_baseline"] = {"value": round(cpu_qps, 1), "unit": "QP/s", "cores": thr, "kind": "port",
+                               "sample": f"{ncpu} instances of this shard (equal per env), oracle/ipm.c "
+                                         f"OpenMP x{thr}, {platform.processor() or platform.machine()}"}
+        I_ref = {k: v[1] for k, v in iref.items()}
+    else:
+        I_ref = {ENVS[j]: float(it_np[offsets[j]:offsets[j + 1]].mean()) for j in range(len(ENVS))}
+    flops_step = sum(seg[j] * I_ref[ENVS[j]] * probs[j].canonical_flops_per_iter() for j in range(len(ENVS)))
+    achieved = flops_step / (kern_ms * 1e-3) / 1e12
+    bytes_step = args.per_gpu * (32 + 4 + 8 * 40 + 4 + 4)     # x0 + env in; u + status + iters out
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            traffic = tj.get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
+    out["roofline"] = {"bound": "mfma", "compute": "fp64 FMA (vector; FP64 vector peak == FP64 matrix peak)",
+                       "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": traffic,
+                       "kernel_ms_per_step": round(kern_ms, 4), "canonical_flops_per_step": flops_step,
+                       "I_ref": I_ref, "algorithmic_hbm_GBps": round(bytes_step / (kern_ms * 1e-3) / 1e9, 3)}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,390 @@
+// capi.hip -- the extern "C" boundary declared in include/carmpc.h.
+//
+// Setup (carmpc_problem_create) mirrors MPC.__init__ (lib/mpc.py:22-117): the
+// caller passes the discretised model, costs, DARE terminal cost and the
+// constraint half-spaces; the device assembly kernel builds the condensed QP
+// (matrix_gen.py:6-72, mpc.py:196-253).  The solve path (carmpc_solve_batch)
+// replaces cp.Problem(...).solve() of mpc.py:334-335 / 477-478.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "carmpc_internal.h"
+
+using namespace carmpc;
+
+struct carmpc_problem {
+    DevProblem dev{};
+    int device = 0;
+    int nx = NX;
+    int p_all = 0;        // rows before normalisation (assembled problems)
+    bool assembled = false;
+    std::vector<void*> allocs;
+    // assembled full matrices (device), for carmpc_problem_get
+    double *T = nullptr, *S = nullptr, *H = nullptr, *h = nullptr, *G_all = nullptr, *E_all = nullptr,
+           *w0_all = nullptr;
+    ~carmpc_problem() {
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <class T_>
+    hipError_t alloc(T_** ptr, size_t count) {
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T_));
+        if (e == hipSuccess) {
+            allocs.push_back(p);
+            *ptr = static_cast<T_*>(p);
+        }
+        return e;
+    }
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hipfail(hipError_t e, const char* what) {
+    g_err = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    return CARMPC_EHIP;
+}
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t _e = (expr);                      \
+        if (_e != hipSuccess) return hipfail(_e, what); \
+    } while (0)
+
+template <class T_>
+hipError_t upload(carmpc_problem* P, T_** dst, const T_* src, size_t count) {
+    hipError_t e = P->alloc(dst, count);
+    if (e != hipSuccess) return e;
+    if (count && src) e = hipMemcpy(*dst, src, count * sizeof(T_), hipMemcpyHostToDevice);
+    return e;
+}
+
+Settings make_settings(const carmpc_settings* s) {
+    Settings out{1e-10, 1e-12, 60, 0};
+    if (s) {
+        if (s->tol > 0) out.tol = s->tol;
+        if (s->tol_mu > 0) out.tol_mu = s->tol_mu;
+        if (s->max_iter > 0) out.max_iter = s->max_iter;
+        out.kernel = s->kernel;
+    }
+    return out;
+}
+
+// Split rows into QP rows (nonzero G_r) and x0-only rows, given host row norms.
+void classify(const std::vector<double>& nrm, std::vector<int32_t>& qp, std::vector<int32_t>& pre) {
+    double mx = 0.0;
+    for (double v : nrm) mx = std::max(mx, v);
+    const double thr = ZERO_ROW * mx;
+    for (size_t r = 0; r < nrm.size(); ++r) (nrm[r] > thr ? qp : pre).push_back((int32_t)r);
+}
+
+// Upload the per-variable arrays padded to nv (H: identity on the pad; hq rows 0;
+// box [-1,1] on the pad so padded variables sit at 0).
+int finish_padded(carmpc_problem* P, const double* H, const double* hq, const double* lb, const double* ub,
+                  const double* goal) {
+    const int n = P->dev.n, nv = P->dev.nv;
+    std::vector<double> Hp((size_t)nv * nv, 0.0), hqp((size_t)nv * NX, 0.0), lbp(nv, -1.0), ubp(nv, 1.0);
+    for (int i = 0; i < nv; ++i)
+        for (int j = 0; j < nv; ++j)
+            Hp[(size_t)i * nv + j] = (i < n && j < n) ? 0.5 * (H[(size_t)i * n + j] + H[(size_t)j * n + i])
+                                                      : (i == j ? 1.0 : 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < NX; ++k) hqp[(size_t)i * NX + k] = hq[(size_t)i * NX + k];
+    if (lb && ub)
+        for (int i = 0; i < n; ++i) { lbp[i] = lb[i]; ubp[i] = ub[i]; }
+    double *dH, *dhq, *dlb, *dub, *dgoal;
+    HIP_TRY(upload(P, &dH, Hp.data(), Hp.size()), "upload H");
+    HIP_TRY(upload(P, &dhq, hqp.data(), hqp.size()), "upload hq");
+    HIP_TRY(upload(P, &dlb, lbp.data(), lbp.size()), "upload lb");
+    HIP_TRY(upload(P, &dub, ubp.data(), ubp.size()), "upload ub");
+    HIP_TRY(upload(P, &dgoal, goal, NX), "upload goal");
+    P->dev.H = dH; P->dev.hq = dhq; P->dev.lb = dlb; P->dev.ub = dub; P->dev.goal = dgoal;
+    P->dev.boxed = (lb && ub) ? 1 : 0;
+    return CARMPC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char* carmpc_last_error(void) { return g_err.c_str(); }
+const char* carmpc_version(void) { return "carmpc-mi355x 0.1 (gfx950, dense IPM v1)"; }
+
+double carmpc_canonical_flops_per_iter(int32_t n, int32_t p) {
+    const double N_ = n, P_ = p;
+    return P_ * N_ * N_ + N_ * N_ * N_ / 3.0 + 6.0 * N_ * N_ + 12.0 * P_ * N_;
+}
+
+int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
+    if (!d || !out) return fail(CARMPC_EINVAL, "null argument");
+    *out = nullptr;
+    if (d->nx != NX) return fail(CARMPC_EUNSUPPORTED, "nx must be 4 (kinematic bicycle state)");
+    if (d->nu < 1 || d->nu > 4) return fail(CARMPC_EUNSUPPORTED, "nu must be in [1,4]");
+    if (d->N < 1 || d->N > 32) return fail(CARMPC_EUNSUPPORTED, "N must be in [1,32]");
+    if (!d->A || !d->B || !d->Q || !d->R || !d->P || !d->goal) return fail(CARMPC_EINVAL, "null model matrix");
+    if (d->n_state_rows < 0 || d->n_term_rows < 0) return fail(CARMPC_EINVAL, "negative row count");
+    if ((d->n_state_rows && (!d->state_A || !d->state_b)) || (d->n_term_rows && (!d->term_A || !d->term_b)))
+        return fail(CARMPC_EINVAL, "null constraint rows");
+    if ((d->u_lower == nullptr) != (d->u_upper == nullptr)) return fail(CARMPC_EINVAL, "u_lower/u_upper mismatch");
+    const int N = d->N, nu = d->nu, n = N * nu;
+    const int nv = dense_pick_nv(n);
+    if (nv < 0) return fail(CARMPC_EUNSUPPORTED, "N*nu must be <= 64");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto* P = new carmpc_problem();
+    P->device = dev;
+    P->assembled = true;
+    const int nt = d->n_term_rows, ns = d->n_state_rows;
+    const int p_all = nt + ns * N;
+    P->p_all = p_all;
+    AsmArgs a{};
+    a.N = N; a.nu = nu; a.n = n; a.nt = nt; a.ns = ns;
+    double *dA, *dB, *dQ, *dR, *dP, *dtA, *dtb, *dsA, *dsb;
+    hipError_t e;
+#define UP(dst, src, cnt)                                             \
+    if ((e = upload(P, &dst, src, cnt)) != hipSuccess) {              \
+        delete P;                                                     \
+        return hipfail(e, "upload " #src);                            \
+    }
+    UP(dA, d->A, NX * NX); UP(dB, d->B, NX * nu); UP(dQ, d->Q, NX * NX); UP(dR, d->R, nu * nu);
+    UP(dP, d->P, NX * NX); UP(dtA, d->term_A, (size_t)nt * NX); UP(dtb, d->term_b, nt);
+    UP(dsA, d->state_A, (size_t)ns * NX); UP(dsb, d->state_b, ns);
+#undef UP
+    double *rownorm, *Phi, *coef;
+    int32_t* stage;
+    if ((e = P->alloc(&P->T, (size_t)(N + 1) * NX * NX)) != hipSuccess ||
+        (e = P->alloc(&P->S, (size_t)(N + 1) * NX * n)) != hipSuccess ||
+        (e = P->alloc(&P->H, (size_t)n * n)) != hipSuccess || (e = P->alloc(&P->h, (size_t)n * NX)) != hipSuccess ||
+        (e = P->alloc(&P->G_all, (size_t)p_all * n)) != hipSuccess ||
+        (e = P->alloc(&P->E_all, (size_t)p_all * NX)) != hipSuccess ||
+        (e = P->alloc(&P->w0_all, (size_t)p_all)) != hipSuccess || (e = P->alloc(&rownorm, (size_t)p_all)) != hipSuccess ||
+        (e = P->alloc(&Phi, (size_t)N * NX * nu)) != hipSuccess || (e = P->alloc(&coef, (size_t)p_all * NX)) != hipSuccess ||
+        (e = P->alloc(&stage, (size_t)p_all)) != hipSuccess) {
+        delete P;
+        return hipfail(e, "hipMalloc (assembly)");
+    }
+    a.A = dA; a.B = dB; a.Q = dQ; a.R = dR; a.P = dP;
+    a.term_A = dtA; a.term_b = dtb; a.state_A = dsA; a.state_b = dsb;
+    a.T = P->T; a.S = P->S; a.H = P->H; a.h = P->h; a.G = P->G_all; a.E = P->E_all; a.w0 = P->w0_all;
+    a.rownorm = rownorm; a.Phi = Phi; a.row_stage = stage; a.row_coef = coef;
+    if ((e = launch_assembly(a, nullptr)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) {
+        delete P;
+        return hipfail(e, "assembly kernel");
+    }
+    std::vector<double> nrm(p_all), Hh((size_t)n * n), hh((size_t)n * NX);
+    if ((e = hipMemcpy(nrm.data(), rownorm, sizeof(double) * p_all, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(Hh.data(), P->H, sizeof(double) * n * n, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(hh.data(), P->h, sizeof(double) * n * NX, hipMemcpyDeviceToHost)) != hipSuccess) {
+        delete P;
+        return hipfail(e, "readback");
+    }
+    std::vector<int32_t> qp, pre;
+    classify(nrm, qp, pre);
+    DevProblem& D = P->dev;
+    D.n = n; D.nv = nv; D.p = (int)qp.size(); D.npre = (int)pre.size(); D.ldg = nv + 2; D.N = N; D.nu = nu;
+    size_t lds = 0;
+    if (!dense_supported(nv, D.p, &lds)) {
+        delete P;
+        return fail(CARMPC_EUNSUPPORTED, "problem too large for the LDS-resident dense kernel (p=" +
+                                             std::to_string(D.p) + ", n=" + std::to_string(n) + ")");
+    }
+    int32_t *dqp, *dpre, *stagep;
+    double *Gp, *Ep, *w0p, *prew, *preE, *coefp;
+    if ((e = upload(P, &dqp, qp.data(), qp.size())) != hipSuccess ||
+        (e = upload(P, &dpre, pre.data(), pre.size())) != hipSuccess ||
+        (e = P->alloc(&Gp, (size_t)D.p * D.ldg)) != hipSuccess || (e = P->alloc(&Ep, (size_t)D.p * NX)) != hipSuccess ||
+        (e = P->alloc(&w0p, (size_t)D.p)) != hipSuccess || (e = P->alloc(&prew, (size_t)D.npre)) != hipSuccess ||
+        (e = P->alloc(&preE, (size_t)D.npre * NX)) != hipSuccess || (e = P->alloc(&coefp, (size_t)D.p * NX)) != hipSuccess ||
+        (e = P->alloc(&stagep, (size_t)D.p)) != hipSuccess) {
+        delete P;
+        return hipfail(e, "hipMalloc (pack)");
+    }
+    PackArgs pk{};
+    pk.n = n; pk.nv = nv; pk.ldg = D.ldg; pk.p = D.p; pk.npre = D.npre; pk.p_all = p_all;
+    pk.qp_rows = dqp; pk.pre_rows = dpre; pk.G = P->G_all; pk.E = P->E_all; pk.w0 = P->w0_all; pk.rownorm = rownorm;
+    pk.row_coef = coef; pk.row_stage = stage; pk.Gp = Gp; pk.Ep = Ep; pk.w0p = w0p; pk.pre_w0 = prew; pk.pre_E = preE;
+    pk.coefp = coefp; pk.stagep = stagep;
+    if ((D.p + D.npre) > 0 && ((e = launch_pack(pk, nullptr)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)) {
+        delete P;
+        return hipfail(e, "pack kernel");
+    }
+    D.G = Gp; D.E = Ep; D.w0 = w0p; D.pre_w0 = prew; D.pre_E = preE; D.row_coef = coefp; D.row_stage = stagep;
+    D.Phi = Phi; D.A = dA; D.B = dB;
+    // box: tile u_lower/u_upper over the horizon (mpc.py:217-218)
+    std::vector<double> lbv, ubv;
+    if (d->u_lower) {
+        lbv.resize(n); ubv.resize(n);
+        for (int k = 0; k < N; ++k)
+            for (int c = 0; c < nu; ++c) { lbv[k * nu + c] = d->u_lower[c]; ubv[k * nu + c] = d->u_upper[c]; }
+    }
+    int rc = finish_padded(P, Hh.data(), hh.data(), d->u_lower ? lbv.data() : nullptr, d->u_lower ? ubv.data() : nullptr,
+                       d->goal);
+    if (rc != CARMPC_OK) {
+        delete P;
+        return rc;
+    }
+    *out = P;
+    return CARMPC_OK;
+}
+
+int carmpc_problem_create_dense(int32_t n, int32_t p, int32_t nx, const double* H, const double* G, const double* w0,
+                                const double* E, const double* hq, const double* lb, const double* ub,
+                                const double* goal, carmpc_problem** out) {
+    if (!out || !H || !hq || !goal || (p > 0 && (!G || !w0 || !E))) return fail(CARMPC_EINVAL, "null argument");
+    *out = nullptr;
+    if (nx != NX) return fail(CARMPC_EUNSUPPORTED, "nx must be 4");
+    if (n < 1 || p < 0) return fail(CARMPC_EINVAL, "bad sizes");
+    if ((lb == nullptr) != (ub == nullptr)) return fail(CARMPC_EINVAL, "lb/ub mismatch");
+    const int nv = dense_pick_nv(n);
+    if (nv < 0) return fail(CARMPC_EUNSUPPORTED, "n must be <= 64");
+    std::vector<double> nrm(p);
+    for (int r = 0; r < p; ++r) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += G[(size_t)r * n + j] * G[(size_t)r * n + j];
+        nrm[r] = std::sqrt(s);
+    }
+    std::vector<int32_t> qp, pre;
+    classify(nrm, qp, pre);
+    auto* P = new carmpc_problem();
+    HIP_TRY(hipGetDevice(&P->device), "hipGetDevice");
+    DevProblem& D = P->dev;
+    D.n = n; D.nv = nv; D.p = (int)qp.size(); D.npre = (int)pre.size(); D.ldg = nv + 2; D.N = 0; D.nu = 0;
+    size_t lds = 0;
+    if (!dense_supported(nv, D.p, &lds)) {
+        delete P;
+        return fail(CARMPC_EUNSUPPORTED, "problem too large for the LDS-resident dense kernel");
+    }
+    std::vector<double> Gp((size_t)D.p * D.ldg, 0.0), w0p(D.p), Ep((size_t)D.p * NX), prew(D.npre), preE((size_t)D.npre * NX);
+    for (int r = 0; r < D.p; ++r) {
+        const int s = qp[r];
+        for (int j = 0; j < n; ++j) Gp[(size_t)r * D.ldg + j] = G[(size_t)s * n + j] / nrm[s];
+        w0p[r] = w0[s] / nrm[s];
+        for (int k = 0; k < NX; ++k) Ep[(size_t)r * NX + k] = E[(size_t)s * NX + k] / nrm[s];
+    }
+    for (int r = 0; r < D.npre; ++r) {
+        prew[r] = w0[pre[r]];
+        for (int k = 0; k < NX; ++k) preE[(size_t)r * NX + k] = E[(size_t)pre[r] * NX + k];
+    }
+    double *dG, *dw0, *dE, *dprew, *dpreE;
+    hipError_t e;
+    if ((e = upload(P, &dG, Gp.data(), Gp.size())) != hipSuccess || (e = upload(P, &dw0, w0p.data(), w0p.size())) != hipSuccess ||
+        (e = upload(P, &dE, Ep.data(), Ep.size())) != hipSuccess || (e = upload(P, &dprew, prew.data(), prew.size())) != hipSuccess ||
+        (e = upload(P, &dpreE, preE.data(), preE.size())) != hipSuccess) {
+        delete P;
+        return hipfail(e, "upload dense problem");
+    }
+    D.G = dG; D.w0 = dw0; D.E = dE; D.pre_w0 = dprew; D.pre_E = dpreE;
+    int rc = finish_padded(P, H, hq, lb, ub, goal);
+    if (rc != CARMPC_OK) {
+        delete P;
+        return rc;
+    }
+    *out = P;
+    return CARMPC_OK;
+}
+
+void carmpc_problem_destroy(carmpc_problem* prob) { delete prob; }
+
+int carmpc_problem_info(const carmpc_problem* P, int32_t* n, int32_t* p, int32_t* npre, int32_t* nx, int32_t* N) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    if (n) *n = P->dev.n;
+    if (p) *p = P->dev.p;
+    if (npre) *npre = P->dev.npre;
+    if (nx) *nx = NX;
+    if (N) *N = P->dev.N;
+    return CARMPC_OK;
+}
+
+int carmpc_problem_get(const carmpc_problem* P, double* T, double* S, double* H, double* h, double* G, double* E,
+                       double* w0, int32_t* p_all) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    if (!P->assembled) return fail(CARMPC_EINVAL, "not an assembled problem");
+    const int N = P->dev.N, n = P->dev.n, pa = P->p_all;
+    if (p_all) *p_all = pa;
+    struct Item { void* dst; const void* src; size_t bytes; } items[] = {
+        {T, P->T, sizeof(double) * (N + 1) * NX * NX}, {S, P->S, sizeof(double) * (N + 1) * NX * n},
+        {H, P->H, sizeof(double) * n * n},             {h, P->h, sizeof(double) * n * NX},
+        {G, P->G_all, sizeof(double) * pa * n},        {E, P->E_all, sizeof(double) * pa * NX},
+        {w0, P->w0_all, sizeof(double) * pa}};
+    for (auto& it : items)
+        if (it.dst && it.bytes) HIP_TRY(hipMemcpy(it.dst, it.src, it.bytes, hipMemcpyDeviceToHost), "problem_get");
+    return CARMPC_OK;
+}
+
+int carmpc_solve_batch(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref, double* u_out,
+                       int32_t* status, int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    if (batch < 0) return fail(CARMPC_EINVAL, "negative batch");
+    if (batch == 0) return CARMPC_OK;
+    if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
+    const Settings s = make_settings(settings);
+    int unsupported = 0;
+    hipError_t e = launch_dense(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
+    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+    if (e != hipSuccess) return hipfail(e, "solve launch");
+    return CARMPC_OK;
+}
+
+int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, const int64_t* offsets,
+                          const double* x0, const double* xref, double* u_out, int64_t ld_u, int32_t* status,
+                          int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
+    if (!probs || !offsets || nprobs < 0) return fail(CARMPC_EINVAL, "null argument");
+    const Settings s = make_settings(settings);
+    for (int j = 0; j < nprobs; ++j) {
+        const int64_t b0 = offsets[j], b1 = offsets[j + 1];
+        if (b1 < b0) return fail(CARMPC_EINVAL, "offsets must be non-decreasing");
+        if (b1 == b0) continue;
+        const carmpc_problem* P = probs[j];
+        if (!P) return fail(CARMPC_EINVAL, "null problem in segment list");
+        if (ld_u < P->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
+        int unsupported = 0;
+        hipError_t e = launch_dense(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
+                                    ld_u, status + b0, iters ? iters + b0 : nullptr, s, stream, &unsupported);
+        if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+        if (e != hipSuccess) return hipfail(e, "segment launch");
+    }
+    return CARMPC_OK;
+}
+
+int carmpc_observer_batch(const carmpc_problem* P, int64_t batch, const double* y, int32_t ny, const double* C,
+                          const double* L, double* xhat, const double* uprev, int64_t ld_uprev, hipStream_t stream) {
+    if (!P || !y || !C || !L || !xhat || !uprev) return fail(CARMPC_EINVAL, "null argument");
+    if (!P->assembled) return fail(CARMPC_EINVAL, "observer needs an assembled problem (A, B)");
+    if (ny < 1 || ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
+    // C and L are tiny host arrays: stage them in a per-thread device cache.
+    thread_local double* dCL = nullptr;
+    thread_local int dev_of = -1;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    if (!dCL || dev_of != dev) {
+        HIP_TRY(hipMalloc(&dCL, sizeof(double) * 2 * 8 * NX), "hipMalloc observer");
+        dev_of = dev;
+    }
+    std::vector<double> host(2 * 8 * NX, 0.0);
+    std::memcpy(host.data(), C, sizeof(double) * ny * NX);
+    std::memcpy(host.data() + 8 * NX, L, sizeof(double) * NX * ny);
+    HIP_TRY(hipMemcpyAsync(dCL, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice, stream), "copy C,L");
+    HIP_TRY(hipStreamSynchronize(stream), "sync C,L");
+    ObsArgs a{};
+    a.batch = batch; a.ny = ny; a.nu = P->dev.nu; a.ld_uprev = ld_uprev;
+    a.A = P->dev.A; a.B = P->dev.B; a.C = dCL; a.L = dCL + 8 * NX; a.y = y; a.uprev = uprev; a.xhat = xhat;
+    HIP_TRY(launch_observer(a, stream), "observer launch");
+    return CARMPC_OK;
+}
+
+int carmpc_plant_step_batch(int64_t batch, double* state, const double* u, int64_t ld_u, double dt, double l1,
+                            int32_t* bad, hipStream_t stream) {
+    if (batch < 0 || (batch > 0 && (!state || !u))) return fail(CARMPC_EINVAL, "bad argument");
+    HIP_TRY(launch_plant(batch, state, u, ld_u, dt, l1, bad, stream), "plant launch");
+    return CARMPC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// carmpc_internal.h -- device-side problem layout shared by the HIP kernels and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/carmpc.h"
+
+namespace carmpc {
+
+constexpr int NX = 4;                 // bicycle state dimension (mpc.py:59)
+constexpr double UNBOXED_BOUND = 1e9; // |u_i| assumed by the Farkas test for unboxed variables
+constexpr double PRE_TOL = 1e-9;      // x0-only row tolerance
+constexpr double STEP_FRAC = 0.99;
+constexpr double ZERO_ROW = 1e-12;    // relative row-norm threshold for x0-only rows
+
+// Everything a solve kernel reads, as device pointers.  Lives in the problem
+// handle; passed to kernels by value.
+struct DevProblem {
+    int32_t n;      // decision variables (N*nu)
+    int32_t nv;     // kernel width (n padded up to a compiled size)
+    int32_t p;      // normalised QP rows
+    int32_t npre;   // x0-only rows (G_r == 0)
+    int32_t ldg;    // row stride of G in doubles (nv + 2: 16B-aligned, conflict-free)
+    int32_t boxed;  // input box present
+    int32_t N, nu;
+    const double* G;      // p x ldg, unit-norm rows, padded columns 0
+    const double* H;      // nv x nv (padded diagonal 1)
+    const double* w0;     // p
+    const double* E;      // p x NX
+    const double* pre_w0; // npre
+    const double* pre_E;  // npre x NX
+    const double* hq;     // nv x NX
+    const double* lb;     // nv
+    const double* ub;     // nv
+    const double* goal;   // NX
+    const double* A;      // NX x NX
+    const double* B;      // NX x nu
+    // stage structure (staged kernel): row r acts on x_{stage[r]} with coef[r]
+    const int32_t* row_stage; // p
+    const double* row_coef;   // p x NX (normalised with the row)
+    const double* Phi;        // N x NX x nu : Phi_m = A^m B
+};
+
+struct Settings {
+    double tol, tol_mu;
+    int32_t max_iter;
+    int32_t kernel;
+};
+
+
+// Argument blocks of the setup kernels (assembly.hip).
+struct AsmArgs {
+    int N, nu, n, nt, ns;
+    const double *A, *B, *Q, *R, *P;   // NX*NX, NX*nu, NX*NX, nu*nu, NX*NX
+    const double *term_A, *term_b;     // nt*NX, nt
+    const double *state_A, *state_b;   // ns*NX, ns
+    double *T, *S, *H, *h;             // (N+1)NX*NX, (N+1)NX*n, n*n, n*NX
+    double *G, *E, *w0, *rownorm;      // p_all*n, p_all*NX, p_all, p_all
+    double* Phi;                       // N*NX*nu
+    int32_t* row_stage;                // p_all
+    double* row_coef;                  // p_all*NX
+};
+struct PackArgs {
+    int n, nv, ldg, p, npre, p_all;
+    const int32_t* qp_rows;   // p indices into the assembled rows
+    const int32_t* pre_rows;  // npre
+    const double *G, *E, *w0, *rownorm, *row_coef;
+    const int32_t* row_stage;
+    double *Gp, *Ep, *w0p, *pre_w0, *pre_E, *coefp;
+    int32_t* stagep;
+};
+struct ObsArgs {
+    int64_t batch;
+    int ny, nu;
+    int64_t ld_uprev;
+    const double *A, *B, *C, *L;   // device: NX*NX, NX*nu, ny*NX, NX*ny
+    const double* y;
+    const double* uprev;
+    double* xhat;
+};
+hipError_t launch_assembly(const AsmArgs& a, hipStream_t s);
+hipError_t launch_pack(const PackArgs& a, hipStream_t s);
+hipError_t launch_observer(const ObsArgs& a, hipStream_t s);
+hipError_t launch_plant(int64_t batch, double* state, const double* u, int64_t ld_u, double dt, double l1,
+                        int32_t* bad, hipStream_t s);
+
+// Solve-kernel launch helpers (ipm_dense.hip).
+hipError_t launch_dense(const DevProblem& P, int64_t batch, const double* x0, const double* xref,
+                        double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
+                        const Settings& s, hipStream_t stream, int* unsupported);
+bool dense_supported(int nv, int p, size_t* lds_bytes);
+int dense_pick_nv(int n);
+
+}  // namespace carmpc

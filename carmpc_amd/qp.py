@@ -1,0 +1,235 @@
+"""Batched condensed-QP problems on the GPU (thin wrapper over the C ABI).
+
+One ``QPProblem`` = one environment / horizon / linearisation point, i.e. the
+data ``MPC.__init__`` builds (lib/mpc.py:22-117).  Solving replaces the
+per-step ``cp.Problem(...).solve()`` of lib/mpc.py:334-335 and 477-478 for a
+whole batch of states at once.  torch-ROCm tensors are used only as device
+buffers; all arithmetic runs in the HIP kernels of ``csrc/``.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native
+from ._native import CarMPCNativeError, ModelDesc, Settings, check
+
+NX = 4
+
+
+def _dptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _f64(a) -> np.ndarray | None:
+    if a is None:
+        return None
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def _tptr(t: torch.Tensor | None):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(stream: torch.cuda.Stream | None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_gpu(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise CarMPCNativeError("carmpc_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                "there is no CPU fallback")
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    return dev
+
+
+@dataclass
+class SolverSettings:
+    """carmpc_settings; defaults match oracle/qp.py."""
+    tol: float = 1e-10
+    tol_mu: float = 1e-12
+    max_iter: int = 60
+    kernel: int = 0
+
+    def c(self) -> Settings:
+        return Settings(self.tol, self.tol_mu, self.max_iter, self.kernel)
+
+
+class QPProblem:
+    """Device-resident condensed QP of one linear-MPC configuration.
+
+        min 1/2 u'Hu + (h (x0 - xref))'u
+        s.t. G u <= w0 - E x0   (terminal rows on x_N, state rows on x_1..x_N)
+             lb <= u <= ub      (input box, optional)
+    """
+
+    def __init__(self, *, N: int, A, B, Q, R, P, goal, state_A=None, state_b=None, term_A=None, term_b=None,
+                 u_lower=None, u_upper=None, device=None):
+        self.device = require_gpu(device)
+        lib = _native.load()
+        A, B, Q, R, P, goal = (_f64(v) for v in (A, B, Q, R, P, goal))
+        nu = B.shape[1]
+        sA = _f64(state_A if state_A is not None else np.zeros((0, NX)))
+        sb = _f64(state_b if state_b is not None else np.zeros(0))
+        tA = _f64(term_A if term_A is not None else np.zeros((0, NX)))
+        tb = _f64(term_b if term_b is not None else np.zeros(0))
+        lo, hi = _f64(u_lower), _f64(u_upper)
+        self._keep = (A, B, Q, R, P, goal, sA, sb, tA, tb, lo, hi)
+        d = ModelDesc(N=N, nx=NX, nu=nu, A=_dptr(A), B=_dptr(B), Q=_dptr(Q), R=_dptr(R), P=_dptr(P),
+                      n_state_rows=sA.shape[0], state_A=_dptr(sA), state_b=_dptr(sb),
+                      n_term_rows=tA.shape[0], term_A=_dptr(tA), term_b=_dptr(tb),
+                      u_lower=_dptr(lo), u_upper=_dptr(hi), goal=_dptr(goal))
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.carmpc_problem_create(ctypes.byref(d), ctypes.byref(handle)), "carmpc_problem_create")
+        self._h = handle
+        self.N, self.nu, self.assembled = N, nu, True
+        self.goal = goal.copy()
+        self._info()
+
+    @classmethod
+    def dense(cls, H, G, w0, E, hq, goal, lb=None, ub=None, device=None) -> "QPProblem":
+        """Generic dense QP without stage structure (carmpc_problem_create_dense)."""
+        self = cls.__new__(cls)
+        self.device = require_gpu(device)
+        lib = _native.load()
+        H, G, w0, E, hq, goal, lb, ub = (_f64(v) for v in (H, G, w0, E, hq, goal, lb, ub))
+        n = H.shape[0]
+        p = 0 if G is None else G.shape[0]
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.carmpc_problem_create_dense(n, p, NX, _dptr(H), _dptr(G), _dptr(w0), _dptr(E), _dptr(hq),
+                                                  _dptr(lb), _dptr(ub), _dptr(goal), ctypes.byref(handle)),
+                  "carmpc_problem_create_dense")
+        self._h = handle
+        self.N, self.nu, self.assembled = None, None, False
+        self.goal = goal.copy()
+        self._keep = ()
+        self._info()
+        return self
+
+    def _info(self):
+        vals = [ctypes.c_int32() for _ in range(5)]
+        check(_native.load().carmpc_problem_info(self._h, *[ctypes.byref(v) for v in vals]), "carmpc_problem_info")
+        self.n, self.p, self.npre, self.nx, _ = (v.value for v in vals)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _native.load().carmpc_problem_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------------ data
+    def matrices(self) -> dict:
+        """Assembled T, S, H, h, G, E, w0 (device assembly kernel output) as numpy."""
+        if not self.assembled:
+            raise ValueError("only assembled problems keep T/S/G")
+        N, n = self.N, self.n
+        pa = ctypes.c_int32()
+        check(_native.load().carmpc_problem_get(self._h, None, None, None, None, None, None, None,
+                                                ctypes.byref(pa)), "carmpc_problem_get")
+        out = dict(T=np.zeros(((N + 1) * NX, NX)), S=np.zeros(((N + 1) * NX, n)), H=np.zeros((n, n)),
+                   h=np.zeros((n, NX)), G=np.zeros((pa.value, n)), E=np.zeros((pa.value, NX)),
+                   w0=np.zeros(pa.value))
+        check(_native.load().carmpc_problem_get(self._h, *[_dptr(out[k]) for k in ("T", "S", "H", "h", "G", "E",
+                                                                                     "w0")], ctypes.byref(pa)),
+              "carmpc_problem_get")
+        return out
+
+    def canonical_flops_per_iter(self) -> float:
+        """p n^2 + n^3/3 + 6 n^2 + 12 p n with p = general (QP) rows."""
+        return float(_native.load().carmpc_canonical_flops_per_iter(self.n, self.p))
+
+    # ----------------------------------------------------------------- solve
+    def solve(self, x0: torch.Tensor, xref: torch.Tensor | None = None, settings: SolverSettings | None = None,
+              out: tuple | None = None, stream=None):
+        """Solve QP(x0) for every row of x0 (B x 4, float64, on this problem's device).
+
+        Returns (u (B x n) float64, status (B,) int32, iters (B,) int32), all on device;
+        stream-ordered, no host synchronisation."""
+        x0 = _as_dev(x0, self.device)
+        B = x0.shape[0]
+        if xref is not None:
+            xref = _as_dev(xref, self.device)
+            if xref.shape != x0.shape:
+                raise ValueError("xref must have the shape of x0")
+        if out is None:
+            u = torch.empty((B, self.n), dtype=torch.float64, device=self.device)
+            st = torch.empty(B, dtype=torch.int32, device=self.device)
+            it = torch.empty(B, dtype=torch.int32, device=self.device)
+        else:
+            u, st, it = out
+        s = (settings or SolverSettings()).c()
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_solve_batch(self._h, B, _tptr(x0), _tptr(xref), _tptr(u), _tptr(st),
+                                                    _tptr(it), ctypes.byref(s), _stream_handle(stream)),
+                  "carmpc_solve_batch")
+        return u, st, it
+
+    def observe(self, y: torch.Tensor, xhat: torch.Tensor, uprev: torch.Tensor, C, L, stream=None) -> None:
+        """In-place Luenberger update xhat <- A xhat + B uprev + L (y - C xhat) (mpc.py:439-448)."""
+        C, L = _f64(C), _f64(L)
+        y = _as_dev(y, self.device, width=C.shape[0])
+        if xhat.dtype != torch.float64 or not xhat.is_contiguous() or xhat.device != self.device:
+            raise ValueError("xhat must be a contiguous float64 tensor on the problem device")
+        if uprev.dtype != torch.float64 or uprev.stride(1) != 1:
+            raise ValueError("uprev must be float64 with unit column stride")
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_observer_batch(self._h, xhat.shape[0], _tptr(y), C.shape[0], _dptr(C),
+                                                       _dptr(L), _tptr(xhat), _tptr(uprev), uprev.stride(0),
+                                                       _stream_handle(stream)), "carmpc_observer_batch")
+
+
+def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,
+                   settings: SolverSettings | None = None, stream=None):
+    """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j]."""
+    dev = problems[0].device
+    x0 = _as_dev(x0, dev)
+    B = x0.shape[0]
+    ld = max(p.n for p in problems)
+    u = torch.zeros((B, ld), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    handles = (ctypes.c_void_p * len(problems))(*[p._h.value for p in problems])
+    offs = (ctypes.c_int64 * (len(problems) + 1))(*[int(o) for o in offsets])
+    s = (settings or SolverSettings()).c()
+    xr = None if xref is None else _as_dev(xref, dev)
+    with torch.cuda.device(dev):
+        check(_native.load().carmpc_solve_segments(handles, len(problems), offs, _tptr(x0), _tptr(xr), _tptr(u), ld,
+                                                   _tptr(st), _tptr(it), ctypes.byref(s), _stream_handle(stream)),
+              "carmpc_solve_segments")
+    return u, st, it
+
+
+def plant_step(state: torch.Tensor, u: torch.Tensor, dt: float, l1: float, stream=None) -> torch.Tensor:
+    """Batched nonlinear plant (simulator.py:51-69), in place on device.  Returns the per-instance
+    input-limit flags of check_input (simulator.py:83-97); flagged rows are stepped anyway."""
+    if state.dtype != torch.float64 or not state.is_contiguous():
+        raise ValueError("state must be contiguous float64")
+    bad = torch.empty(state.shape[0], dtype=torch.int32, device=state.device)
+    with torch.cuda.device(state.device):
+        check(_native.load().carmpc_plant_step_batch(state.shape[0], _tptr(state), _tptr(u), u.stride(0), dt, l1,
+                                                     _tptr(bad), _stream_handle(stream)), "carmpc_plant_step_batch")
+    return bad
+
+
+def _as_dev(t, device, width: int = NX) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(np.asarray(t, dtype=np.float64))
+    if t.dim() == 1:
+        t = t.reshape(1, -1)
+    t = t.to(device=device, dtype=torch.float64)
+    if not t.is_contiguous():
+        t = t.contiguous()
+    if t.shape[1] != width:
+        raise ValueError(f"expected rows of length {width}, got {tuple(t.shape)}")
+    return t

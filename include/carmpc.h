@@ -1,0 +1,156 @@
+/*
+ * carmpc.h -- C ABI of the MI355X-native batched linear-MPC QP solver.
+ *
+ * Drop-in boundary for the per-step QP of CarMPC's controllers.  In the
+ * reference the boundary is a Python call into cvxpy (no FFI exists):
+ *
+ *   MPC.__init__                lib/mpc.py:22-117   -> carmpc_problem_create (assembly on device)
+ *     predmod / costgen         lib/matrix_gen.py:6-72
+ *     constraint stacks         lib/mpc.py:196-253
+ *   MPCStateFB.step  cp.Problem(...).solve()   lib/mpc.py:318-335  -> carmpc_solve_batch
+ *   MPCOutputFB.step cp.Problem(...).solve()   lib/mpc.py:461-478  -> carmpc_solve_batch
+ *   MPCOutputFB.luenberger_observer            lib/mpc.py:439-448  -> carmpc_observer_batch
+ *   OutsideTheRegionOfAttractionError          lib/mpc.py:17,336-338 -> status CARMPC_PRIMAL_INFEASIBLE
+ *   CarSimulator.step (plant)                  lib/simulator.py:51-69,99-118 -> carmpc_plant_step_batch
+ *
+ * Conventions
+ *   - All matrices are row-major fp64.  Descriptor (host) pointers are read
+ *     during the call only.  Batch pointers (x0, u_out, ...) are DEVICE
+ *     pointers owned by the caller (e.g. torch-ROCm tensors).
+ *   - Every launch is stream-ordered on the given hipStream_t (NULL = default
+ *     stream); no hidden host synchronisation in the solve path.
+ *   - Functions return 0 on success or a negative CARMPC_E* code; the message
+ *     of the last error on the calling thread is available from
+ *     carmpc_last_error().
+ *   - One problem handle per (environment, horizon, linearisation point);
+ *     handles are bound to the device current at creation.
+ */
+#ifndef CARMPC_H
+#define CARMPC_H
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status of one QP instance (int32 per instance) ---------------------- */
+enum {
+    CARMPC_OPTIMAL = 0,            /* KKT residuals within tolerance                    */
+    CARMPC_PRIMAL_INFEASIBLE = 1,  /* certificate found; reference raises               */
+                                   /* OutsideTheRegionOfAttractionError (mpc.py:336-338) */
+    CARMPC_MAX_ITER = 2,
+    CARMPC_NUMERICAL = 3
+};
+
+/* ---- error codes --------------------------------------------------------- */
+enum {
+    CARMPC_OK = 0,
+    CARMPC_EINVAL = -1,     /* bad argument / shape                                    */
+    CARMPC_EUNSUPPORTED = -2, /* size outside the compiled kernel set (e.g. n > 64)    */
+    CARMPC_EHIP = -3,       /* HIP runtime error (message has the hipError_t name)     */
+    CARMPC_ENOMEM = -4
+};
+
+typedef struct carmpc_problem carmpc_problem;
+
+/* Linear-MPC model description: the inputs of MPC.__init__ after linearisation
+ * and discretisation (mpc.py:53-54) and DARE (mpc.py:70).  The library builds
+ * T, S, H = R_hat + S'Q_hat S, h = S'Q_hat T (matrix_gen.py:6-72) and the
+ * stacked constraint rows (mpc.py:196-253) with a device assembly kernel.  */
+typedef struct {
+    int32_t N;            /* horizon (configuration.py:16), 1..32                      */
+    int32_t nx, nu;       /* 4, 2 for the bicycle model                                */
+    const double* A;      /* nx*nx  discrete dynamics (mpc.py:164-180)                 */
+    const double* B;      /* nx*nu                                                     */
+    const double* Q;      /* nx*nx  stage cost (configuration.py:19)                   */
+    const double* R;      /* nu*nu  (configuration.py:21)                              */
+    const double* P;      /* nx*nx  terminal cost (mpc.py:70)                          */
+    int32_t n_state_rows; /* per-step half-spaces c'x_k <= d on x_1..x_N (mpc.py:222-253) */
+    const double* state_A;/* n_state_rows*nx                                           */
+    const double* state_b;/* n_state_rows                                              */
+    int32_t n_term_rows;  /* terminal half-spaces on x_N (mpc.py:96-117), 0 = none      */
+    const double* term_A; /* n_term_rows*nx                                            */
+    const double* term_b; /* n_term_rows                                               */
+    const double* u_lower;/* nu, NULL => no input box (input_constraint=False)         */
+    const double* u_upper;/* nu                                                        */
+    const double* goal;   /* nx  default reference (mpc.py:46,182-194)                 */
+} carmpc_model_desc;
+
+/* Solver settings.  Pass NULL for the defaults
+ * {1e-10, 1e-12, 60}. */
+typedef struct {
+    double tol;        /* primal/dual residual tolerance, relative to 1+||.||_inf */
+    double tol_mu;     /* complementarity tolerance (absolute)                     */
+    int32_t max_iter;
+    int32_t kernel;    /* 0 = auto, 1 = dense (G,H in LDS), 2 = staged (structure) */
+} carmpc_settings;
+
+/* Build one problem on the current device (assembly kernel + row normalisation). */
+int carmpc_problem_create(const carmpc_model_desc* desc, carmpc_problem** out);
+
+/* Generic dense variant (no stage structure): min 1/2u'Hu + (hq(x0-xref))'u
+ * s.t. G u <= w0 - E x0, lb <= u <= ub.  H n*n, G p*n, w0 p, E p*nx, hq n*nx,
+ * lb/ub n (NULL = no box), goal nx.  Host pointers. */
+int carmpc_problem_create_dense(int32_t n, int32_t p, int32_t nx, const double* H, const double* G,
+                                const double* w0, const double* E, const double* hq,
+                                const double* lb, const double* ub, const double* goal,
+                                carmpc_problem** out);
+
+void carmpc_problem_destroy(carmpc_problem* prob);
+
+/* Sizes: n decision variables, p QP rows after normalisation, npre x0-only rows. */
+int carmpc_problem_info(const carmpc_problem* prob, int32_t* n, int32_t* p, int32_t* npre,
+                        int32_t* nx, int32_t* N);
+
+/* Copy assembled matrices back to HOST buffers (any pointer may be NULL):
+ * T (N+1)nx*nx, S (N+1)nx*n, H n*n, h n*nx, G p_all*n, E p_all*nx, w0 p_all
+ * (p_all = rows before normalisation, order: terminal then state blocks as in
+ * mpc.py:323-332).  Only valid for carmpc_problem_create problems. */
+int carmpc_problem_get(const carmpc_problem* prob, double* T, double* S, double* H, double* h,
+                       double* G, double* E, double* w0, int32_t* p_all);
+
+/* Solve B independent QP(x0) instances (MPCStateFB.step semantics, mpc.py:312-349):
+ *   x0    B*nx  device, absolute state (constraints use it as is, mpc.py:319)
+ *   xref  B*nx  device or NULL (NULL = goal; cost uses x0 - xref, mpc.py:320)
+ *   u_out B*n   device, optimal input sequence u_0..u_{N-1}
+ *   status, iters  B int32 device (iters may be NULL)                          */
+int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
+                       double* u_out, int32_t* status, int32_t* iters,
+                       const carmpc_settings* settings, hipStream_t stream);
+
+/* Several problems in one call: instances grouped by problem, segment j is
+ * [offsets[j], offsets[j+1]) (host array of nprobs+1).  Row strides follow
+ * each problem's n; u_out uses a common row stride ld_u >= max n. */
+int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, const int64_t* offsets,
+                          const double* x0, const double* xref, double* u_out, int64_t ld_u,
+                          int32_t* status, int32_t* iters, const carmpc_settings* settings,
+                          hipStream_t stream);
+
+/* Luenberger observer (mpc.py:439-448), in place on device:
+ *   xhat <- A xhat + B uprev + L (y - C xhat)
+ * y B*ny, xhat B*nx, uprev rows at stride ld_uprev (first nu entries used),
+ * C ny*nx, L nx*ny host arrays.  A, B come from the problem. */
+int carmpc_observer_batch(const carmpc_problem* prob, int64_t batch, const double* y, int32_t ny,
+                          const double* C, const double* L, double* xhat, const double* uprev,
+                          int64_t ld_uprev, hipStream_t stream);
+
+/* Nonlinear kinematic bicycle plant, forward Euler (simulator.py:51-69):
+ * state <- state + dt*[v cos psi, v sin psi, v/l1 tan delta, a];
+ * u rows at stride ld_u (first 2 entries).  Returns CARMPC_OK; per-instance
+ * input-limit violations (simulator.py:83-97) are flagged in bad (nullable). */
+int carmpc_plant_step_batch(int64_t batch, double* state, const double* u, int64_t ld_u, double dt,
+                            double l1, int32_t* bad, hipStream_t stream);
+
+/* Canonical per-iteration flop count of the dense condensed IPM
+ * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
+double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);
+
+const char* carmpc_last_error(void);
+const char* carmpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CARMPC_H */

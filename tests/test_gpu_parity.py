@@ -1,0 +1,187 @@
+"""GPU parity: HIP assembly + IPM against the oracle (golden fixtures, C oracle, KKT certificates).
+
+Tolerances:
+  |u_gpu - u*|_inf <= 1e-6   against the KKT-certified optimum
+  constraint violation <= 1e-8, terminal-set rows of x_N <= b + 1e-8
+  status identical to the oracle (optimal vs primal-infeasible), except for
+  instances whose LP feasibility margin is within 1e-7 of the boundary.
+"""
+import numpy as np
+import pytest
+
+from conftest import CONFIGS, GOLDEN, TERMINAL_SETS
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+VIOL_TOL = 1e-8
+
+
+def _setup(name, N, **kw):
+    import torch  # noqa: F401
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS, **kw)
+    rows_A, rows_b = (np.asarray(asm.state_rows_A, float), np.asarray(asm.state_rows_b, float)) \
+        if asm.flags[2] else (None, None)
+    qp = QPProblem(N=N, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=rows_A, state_b=rows_b,
+                   term_A=asm.term_A[:, -4:] if asm.flags[0] else None,
+                   term_b=asm.term_b if asm.flags[0] else None,
+                   u_lower=asm.input_lower if asm.flags[1] else None,
+                   u_upper=asm.input_upper if asm.flags[1] else None)
+    return asm, qp
+
+
+def _violation(asm, x0, u):
+    """max over general rows and box of (A u - b), with the un-normalised reference rows."""
+    w = asm.w0 - asm.E @ x0
+    v = (asm.G @ u - w).max() if len(w) else -np.inf
+    if asm.lb is not None:
+        v = max(v, (u - asm.ub).max(), (asm.lb - u).max())
+    return v
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_assembly_kernel_matches_oracle(gpu_available, name, N):
+    asm, qp = _setup(name, N)
+    m = qp.matrices()
+    for key in ("T", "S"):
+        np.testing.assert_allclose(m[key], getattr(asm, key), rtol=0, atol=1e-13)
+    np.testing.assert_allclose(m["H"], asm.H, rtol=1e-12, atol=1e-10)
+    np.testing.assert_allclose(m["h"], asm.h, rtol=1e-12, atol=1e-10)
+    np.testing.assert_allclose(m["G"], asm.G, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(m["E"], asm.E, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(m["w0"], asm.w0)
+    golden = np.load(f"{GOLDEN}/assembly_{name}_N{N}.npz")
+    np.testing.assert_allclose(m["H"], golden["H"], rtol=1e-12, atol=1e-10)
+    np.testing.assert_allclose(m["S"], golden["S"], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_golden_vectors(gpu_available, name, N):
+    import torch
+    asm, qp = _setup(name, N)
+    g = np.load(f"{GOLDEN}/qp_{name}_N{N}.npz")
+    u, st, it = qp.solve(torch.as_tensor(g["x0"]).cuda())
+    u, st, it = u.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+    np.testing.assert_array_equal(st, g["status"])
+    ok = st == 0
+    assert ok.any()
+    err = np.abs(u[ok] - g["u_star"][ok]).max()
+    assert err <= U_TOL, err
+    for x0, uu in zip(g["x0"][ok], u[ok]):
+        assert _violation(asm, x0, uu) <= VIOL_TOL
+        xN = (asm.T @ x0 + asm.S @ uu)[-4:]
+        tA, tb = asm.term_A[:, -4:], asm.term_b
+        assert (tA @ xN - tb).max() <= VIOL_TOL
+    # the IPM follows the oracle's iteration sequence to within a couple of steps
+    assert np.abs(it[ok] - g["iters"][ok]).max() <= 3
+
+
+def _random_x0(rng, goal_x, B):
+    return np.stack([rng.uniform(goal_x - 25, goal_x, B), rng.uniform(-3, 3, B),
+                     rng.uniform(-np.pi / 8, np.pi / 8, B), rng.uniform(-1, 5, B)], axis=1)
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_random_batch_vs_c_oracle(gpu_available, name, N):
+    import torch
+    from oracle.cpu import CpuProblem
+    from oracle import qp as oq
+    asm, qp = _setup(name, N)
+    rng = np.random.default_rng(11 + N)
+    X = _random_x0(rng, asm.goal[0], 2048)
+    u, st, it = qp.solve(torch.as_tensor(X).cuda())
+    u, st = u.cpu().numpy(), st.cpu().numpy()
+    uc, sc, ic = CpuProblem(asm).solve(X)
+    agree = st == sc
+    if not agree.all():
+        # disagreement only allowed at the feasibility boundary
+        Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
+        for i in np.where(~agree)[0]:
+            m = oq.lp_margin(Gn, w0n - En @ X[i], asm.lb, asm.ub)
+            assert abs(m) < 1e-7, (i, st[i], sc[i], m)
+    both = (st == 0) & (sc == 0)
+    assert np.abs(u[both] - uc[both]).max() <= U_TOL
+    assert (st[sc == 0] != 2).all() and (st != 3).all()
+    # certify a sample against the exact optimum
+    idx = np.where(both)[0][:48]
+    for i in idx:
+        r = oq.solve_instance(asm, X[i])
+        assert r["certified"]
+        assert np.abs(u[i] - r["u_exact"]).max() <= U_TOL
+        assert _violation(asm, X[i], u[i]) <= VIOL_TOL
+
+
+def test_flags_and_edge_cases(gpu_available):
+    import torch
+    from oracle.cpu import CpuProblem
+    rng = np.random.default_rng(5)
+    for kw in (dict(input_constraint_on=False), dict(terminal_constraint=False), dict(state_constraint_on=False)):
+        asm, qp = _setup("RoadEnv", 20, **kw)
+        X = _random_x0(rng, asm.goal[0], 300)
+        u, st, _ = qp.solve(torch.as_tensor(X).cuda())
+        uc, sc, _ = CpuProblem(asm).solve(X)
+        st = st.cpu().numpy()
+        both = (st == 0) & (sc == 0)
+        assert (st == sc).mean() > 0.99, kw
+        assert np.abs(u.cpu().numpy()[both] - uc[both]).max() <= U_TOL, kw
+    # empty batch, single instance, batch not a multiple of the workgroup, x0 at the goal
+    asm, qp = _setup("RoadOneCarEnv", 20)
+    u, st, it = qp.solve(torch.zeros((0, 4), dtype=torch.float64).cuda())
+    assert u.shape == (0, 40)
+    g = torch.as_tensor(asm.goal.reshape(1, 4)).cuda()
+    u, st, it = qp.solve(g)
+    assert int(st[0]) == 0 and float(u.abs().max()) <= 1e-9
+    X = _random_x0(rng, asm.goal[0], 13)
+    u, st, _ = qp.solve(torch.as_tensor(X).cuda())
+    uc, sc, _ = CpuProblem(asm).solve(X)
+    np.testing.assert_array_equal(st.cpu().numpy(), sc)
+    # explicit xref equal to the goal gives the same answer
+    u2, st2, _ = qp.solve(torch.as_tensor(X).cuda(), torch.as_tensor(np.tile(asm.goal, (13, 1))).cuda())
+    assert torch.equal(u, u2) and torch.equal(st, st2)
+
+
+def test_terminal_fallback_and_short_horizon(gpu_available, tmp_path):
+    """Missing terminal-set file -> goal box (mpc.py:107-117); N=5 exercises kernel padding (n=10 -> 16)."""
+    import torch
+    from oracle.cpu import CpuProblem
+    for N in (5, 10):
+        from oracle import assembly as oa
+        asm = oa.build("RoadEnv", N, terminal_set_dir=str(tmp_path))
+        assert asm.term_file is None
+        from carmpc_amd.qp import QPProblem
+        qp = QPProblem(N=N, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                       state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                       term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower,
+                       u_upper=asm.input_upper)
+        rng = np.random.default_rng(N)
+        X = np.stack([rng.uniform(28, 30, 200), rng.uniform(1, 2, 200), rng.uniform(-0.05, 0.05, 200),
+                      rng.uniform(-0.2, 0.2, 200)], axis=1)
+        u, st, _ = qp.solve(torch.as_tensor(X).cuda())
+        uc, sc, _ = CpuProblem(asm).solve(X)
+        st = st.cpu().numpy()
+        assert (st == sc).mean() > 0.99
+        both = (st == 0) & (sc == 0)
+        if both.any():
+            assert np.abs(u.cpu().numpy()[both] - uc[both]).max() <= U_TOL
+
+
+def test_observer_and_plant_kernels(gpu_available):
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd.qp import plant_step
+    asm, qp = _setup("RoadMultipleCarsEnv", 20)
+    rng = np.random.default_rng(3)
+    B = 257
+    xh = rng.normal(size=(B, 4)); up = rng.normal(size=(B, 2)); y = rng.normal(size=(B, 3))
+    xt = torch.as_tensor(xh.copy()).cuda()
+    qp.observe(torch.as_tensor(y).cuda(), xt, torch.as_tensor(up).cuda(), oa.C_OUT, oa.L_OBS)
+    ref = np.stack([oa.luenberger_observer(asm.A, asm.B, xh[i], up[i], y[i]) for i in range(B)])
+    np.testing.assert_allclose(xt.cpu().numpy(), ref, rtol=1e-14, atol=1e-13)
+    g = np.load(f"{GOLDEN}/plant.npz")
+    st = torch.as_tensor(g["state"].copy()).cuda()
+    bad = plant_step(st, torch.as_tensor(g["u"]).cuda(), 0.2, 3.5)
+    np.testing.assert_allclose(st.cpu().numpy(), g["next"], rtol=1e-14, atol=1e-13)
+    assert int(bad.sum()) == 0
