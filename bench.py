@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=24576)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 3 dense 1-wave/SIMD)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -103,7 +104,8 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    from carmpc_amd.qp import solve_segments
+    from carmpc_amd.qp import SolverSettings, solve_segments
+    settings = SolverSettings(kernel=args.kernel)
     ctrls = build_problems(device)
     probs = [c.qp for c in ctrls]
     goals = [c.goal for c in ctrls]
@@ -113,7 +115,7 @@ def main():
 
     stream = torch.cuda.current_stream()
     for _ in range(args.warmup):
-        u, st, it = solve_segments(probs, offsets, Xd, stream=stream)
+        u, st, it = solve_segments(probs, offsets, Xd, settings=settings, stream=stream)
     torch.cuda.synchronize()
 
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -124,7 +126,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev0[k].record(stream)
-        u, st, it = solve_segments(probs, offsets, Xd, stream=stream)
+        u, st, it = solve_segments(probs, offsets, Xd, settings=settings, stream=stream)
         ev1[k].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -141,7 +143,7 @@ def main():
     torch.cuda.synchronize()
     te = time.perf_counter()
     Xe = Xh.to(device, non_blocking=True)
-    ue, se, _ = solve_segments(probs, offsets, Xe, stream=stream)
+    ue, se, _ = solve_segments(probs, offsets, Xe, settings=settings, stream=stream)
     uh = ue.to("cpu"); sh = se.to("cpu")
     torch.cuda.synchronize()
     e2e = args.per_gpu / (time.perf_counter() - te)

@@ -9,9 +9,11 @@
  *     min 1/2 u'Hu + q'u,  q = hq (x0 - xref)          (mpc.py:320-321)
  *     s.t. G u <= w0 - E x0  (terminal + state rows)    (mpc.py:319,324-332)
  *          lb <= u <= ub     (input box)                (mpc.py:327-329)
- * with the dense Mehrotra IPM of DESIGN.md §3 / oracle/qp.py::ipm (same
- * settings, same guard rules), OpenMP over instances.  G/w0/E rows are the
- * normalised QP rows; pre_* are the x0-only rows (G_r == 0), checked first.
+ * with the algorithm of DESIGN.md §3 / oracle/qp.py::ipm: dense Mehrotra
+ * predictor-corrector on the normal equations, one refinement pass on the
+ * corrector, rigorous box-Farkas infeasibility test, and the active-set polish.
+ * OpenMP over instances.  G/w0/E rows are the normalised QP rows; pre_* are
+ * the x0-only rows (G_r == 0), checked first.
  *
  * Status codes: 0 optimal, 1 primal infeasible, 2 max iterations, 3 numerical.
  */
@@ -26,6 +28,15 @@
 #define UNBOXED_BOUND 1e9
 #define PRE_TOL 1e-9
 #define STEP_FRAC 0.99
+#define POLISH_MU 1e-8
+#define POLISH_DELTA 1e-10
+#define POLISH_REFINE 3
+#define POLISH_TOL 1e-11
+
+typedef struct {
+    int n, p, boxed;
+    const double *H, *G, *lb, *ub;
+} qp_t;
 
 static double maxstep(const double* v, const double* dv, int k, double cur) {
     for (int i = 0; i < k; ++i)
@@ -36,44 +47,184 @@ static double maxstep(const double* v, const double* dv, int k, double cur) {
     return cur;
 }
 
-typedef struct {
-    int n, p, boxed;
-    const double *H, *G, *lb, *ub;
-} qp_t;
+/* M = H + G' diag(dg) G + diag(dbox) (lower triangle), then guarded Cholesky in place. */
+static void factor(const qp_t* P, const double* dg, const double* dbox, double* M) {
+    const int n = P->n, p = P->p;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) M[i * n + j] = P->H[i * n + j];
+    for (int r = 0; r < p; ++r) {
+        if (dg[r] == 0.0) continue;
+        const double* g = P->G + r * n;
+        for (int i = 0; i < n; ++i) {
+            double t = dg[r] * g[i];
+            for (int j = 0; j <= i; ++j) M[i * n + j] += t * g[j];
+        }
+    }
+    if (dbox)
+        for (int i = 0; i < n; ++i) M[i * n + i] += dbox[i];
+    for (int k = 0; k < n; ++k) {
+        double piv = M[k * n + k];
+        if (!(piv > 0.0)) piv = 1e128;
+        double lkk = sqrt(piv);
+        M[k * n + k] = lkk;
+        double inv = 1.0 / lkk;
+        for (int i = k + 1; i < n; ++i) M[i * n + k] *= inv;
+        for (int j = k + 1; j < n; ++j) {
+            double ljk = M[j * n + k];
+            for (int i = j; i < n; ++i) M[i * n + j] -= M[i * n + k] * ljk;
+        }
+    }
+}
 
-/* One instance.  work must hold n*n + 17*n + 9*p doubles (WORK_SIZE). */
-static int solve_one(const qp_t* P, const double* q, const double* w, double* u, double* work,
-                     double tol, double tol_mu, int max_iter, int* iters_out) {
+static void chol_solve(const double* L, int n, double* x) {
+    for (int i = 0; i < n; ++i) {
+        double v = x[i];
+        for (int j = 0; j < i; ++j) v -= L[i * n + j] * x[j];
+        x[i] = v / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = x[i];
+        for (int j = i + 1; j < n; ++j) v -= L[j * n + i] * x[j];
+        x[i] = v / L[i * n + i];
+    }
+}
+
+static void gmul(const qp_t* P, const double* x, double* out) { /* out = G x */
+    for (int r = 0; r < P->p; ++r) {
+        double v = 0.0;
+        for (int j = 0; j < P->n; ++j) v += P->G[r * P->n + j] * x[j];
+        out[r] = v;
+    }
+}
+
+static void gtmul(const qp_t* P, const double* y, double* out) { /* out = G' y */
+    for (int i = 0; i < P->n; ++i) out[i] = 0.0;
+    for (int r = 0; r < P->p; ++r) {
+        if (y[r] == 0.0) continue;
+        for (int i = 0; i < P->n; ++i) out[i] += P->G[r * P->n + i] * y[r];
+    }
+}
+
+typedef struct {   /* per-thread scratch */
+    double *M, *s, *z, *rp, *ds, *dz, *dsa, *dza, *t, *rc, *gv, *pv1, *pv2;
+    double *su, *sl, *zu, *zl, *rpu, *rpl, *rd, *du, *dsu, *dsl, *dzu, *dzl, *dsua, *dzua, *dsla, *dzla, *nv1,
+        *nv2, *nv3, *nv4, *nv5;
+    /* polish-only scratch (must not alias IPM state) */
+    double *pdg, *pyg, *pryg, *pgx, *pdbu, *pdbl, *pyu, *pyl, *prhs, *pdx;
+} work_t;
+
+static void work_alloc(work_t* W, int n, int p) {
+    size_t pn = (size_t)(p > 0 ? p : 1), nn = (size_t)(n > 0 ? n : 1);
+    double* base = (double*)malloc(sizeof(double) * (nn * nn + 17 * pn + 28 * nn));
+    W->M = base;
+    double* c = base + nn * nn;
+    double** pv[] = {&W->s, &W->z, &W->rp, &W->ds, &W->dz, &W->dsa, &W->dza, &W->t, &W->rc, &W->gv, &W->pv1, &W->pv2};
+    for (size_t k = 0; k < sizeof(pv) / sizeof(pv[0]); ++k) { *pv[k] = c; c += pn; }
+    c += pn;
+    double** nvp[] = {&W->su, &W->sl, &W->zu, &W->zl, &W->rpu, &W->rpl, &W->rd, &W->du, &W->dsu, &W->dsl, &W->dzu,
+                      &W->dzl, &W->dsua, &W->dzua, &W->dsla, &W->dzla, &W->nv1, &W->nv2, &W->nv3, &W->nv4, &W->nv5};
+    for (size_t k = 0; k < sizeof(nvp) / sizeof(nvp[0]); ++k) { *nvp[k] = c; c += nn; }
+    double** ppv[] = {&W->pdg, &W->pyg, &W->pryg, &W->pgx};
+    for (size_t k = 0; k < sizeof(ppv) / sizeof(ppv[0]); ++k) { *ppv[k] = c; c += pn; }
+    double** pnv[] = {&W->pdbu, &W->pdbl, &W->pyu, &W->pyl, &W->prhs, &W->pdx};
+    for (size_t k = 0; k < sizeof(pnv) / sizeof(pnv[0]); ++k) { *pnv[k] = c; c += nn; }
+}
+
+/* Active-set polish (oracle/qp.py::polish_step).  Returns 1 and writes x if accepted. */
+static int polish(const qp_t* P, const double* q, const double* w, work_t* W, double* x_out) {
+    const int n = P->n, p = P->p, boxed = P->boxed;
+    const double id = 1.0 / POLISH_DELTA;
+    double* dg = W->pdg;   /* 1/delta on active rows */
+    double* yg = W->pyg;
+    double* ryg = W->pryg;
+    double* gx = W->pgx;
+    double* dbu = W->pdbu; double* dbl = W->pdbl;
+    double* yu = W->pyu; double* yl = W->pyl;
+    double* rhs = W->prhs;
+    double* dx = W->pdx;
+    double* x = x_out;
+    double ryu[64], ryl[64], dbox[64];
+    if (n > 64) return 0;
+    for (int r = 0; r < p; ++r) dg[r] = W->s[r] < W->z[r] ? id : 0.0;
+    for (int i = 0; i < n; ++i) {
+        dbu[i] = (boxed && W->su[i] < W->zu[i]) ? id : 0.0;
+        dbl[i] = (boxed && W->sl[i] < W->zl[i]) ? id : 0.0;
+        dbox[i] = dbu[i] + dbl[i];
+    }
+    factor(P, dg, dbox, W->M);   /* M is rebuilt by the IPM before its next use */
+    /* first solve: rx = -q, ry = b on active rows */
+    for (int r = 0; r < p; ++r) ryg[r] = dg[r] != 0.0 ? w[r] : 0.0;
+    for (int i = 0; i < n; ++i) {
+        ryu[i] = dbu[i] != 0.0 ? P->ub[i] : 0.0;
+        ryl[i] = dbl[i] != 0.0 ? -P->lb[i] : 0.0;
+        x[i] = 0.0; yu[i] = 0.0; yl[i] = 0.0;
+    }
+    for (int r = 0; r < p; ++r) yg[r] = 0.0;
+    for (int pass = 0; pass <= POLISH_REFINE; ++pass) {
+        /* rx = -q - H x - A'y  (pass 0: x = y = 0) */
+        for (int i = 0; i < n; ++i) {
+            double v = -q[i];
+            for (int j = 0; j < n; ++j) v -= P->H[i * n + j] * x[j];
+            rhs[i] = v - yu[i] + yl[i];
+        }
+        gtmul(P, yg, dx);
+        for (int i = 0; i < n; ++i) rhs[i] -= dx[i];
+        if (pass > 0) {   /* ry = b - A x on active rows */
+            gmul(P, x, gx);
+            for (int r = 0; r < p; ++r) ryg[r] = dg[r] != 0.0 ? w[r] - gx[r] : 0.0;
+            for (int i = 0; i < n; ++i) {
+                ryu[i] = dbu[i] != 0.0 ? P->ub[i] - x[i] : 0.0;
+                ryl[i] = dbl[i] != 0.0 ? -P->lb[i] + x[i] : 0.0;
+            }
+        }
+        /* K_delta solve: (H + A'A/delta) dx = rx + A' ry/delta ; dy = (A dx - ry)/delta */
+        for (int r = 0; r < p; ++r) gx[r] = dg[r] * ryg[r];
+        gtmul(P, gx, dx);
+        for (int i = 0; i < n; ++i) rhs[i] += dx[i] + dbu[i] * ryu[i] - dbl[i] * ryl[i];
+        memcpy(dx, rhs, sizeof(double) * n);
+        chol_solve(W->M, n, dx);
+        gmul(P, dx, gx);
+        for (int r = 0; r < p; ++r) yg[r] += dg[r] * (gx[r] - ryg[r]);
+        for (int i = 0; i < n; ++i) {
+            yu[i] += dbu[i] * (dx[i] - ryu[i]);
+            yl[i] += dbl[i] * (-dx[i] - ryl[i]);
+            x[i] += dx[i];
+        }
+    }
+    /* accept: primal feasible and dual nonnegative (relative POLISH_TOL) */
+    double wsc = 0.0, ysc = 0.0, viol = -INFINITY, ymin = 0.0;
+    gmul(P, x, gx);
+    for (int r = 0; r < p; ++r) {
+        if (fabs(w[r]) > wsc) wsc = fabs(w[r]);
+        if (gx[r] - w[r] > viol) viol = gx[r] - w[r];
+        if (fabs(yg[r]) > ysc) ysc = fabs(yg[r]);
+        if (yg[r] < ymin) ymin = yg[r];
+    }
+    for (int i = 0; i < n; ++i) {
+        if (!isfinite(x[i])) return 0;
+        if (boxed) {
+            if (fabs(P->ub[i]) > wsc) wsc = fabs(P->ub[i]);
+            if (fabs(P->lb[i]) > wsc) wsc = fabs(P->lb[i]);
+            if (x[i] - P->ub[i] > viol) viol = x[i] - P->ub[i];
+            if (P->lb[i] - x[i] > viol) viol = P->lb[i] - x[i];
+        }
+        if (fabs(yu[i]) > ysc) ysc = fabs(yu[i]);
+        if (fabs(yl[i]) > ysc) ysc = fabs(yl[i]);
+        if (yu[i] < ymin) ymin = yu[i];
+        if (yl[i] < ymin) ymin = yl[i];
+    }
+    return viol <= POLISH_TOL * (1.0 + wsc) && ymin >= -POLISH_TOL * (1.0 + ysc);
+}
+
+static int solve_one(const qp_t* P, const double* q, const double* w, double* u, work_t* W, double tol,
+                     double tol_mu, int max_iter, int* iters_out) {
     const int n = P->n, p = P->p, boxed = P->boxed;
     const int nb = boxed ? n : 0;
-    const double *H = P->H, *G = P->G, *lb = P->lb, *ub = P->ub;
-    double* M = work;               /* n*n */
-    double* su = M + n * n;         /* n each */
-    double* sl = su + n;
-    double* zu = sl + n;
-    double* zl = zu + n;
-    double* rpu = zl + n;
-    double* rpl = rpu + n;
-    double* rd = rpl + n;
-    double* du = rd + n;
-    double* dsu = du + n;
-    double* dsl = dsu + n;
-    double* dzu = dsl + n;
-    double* dzl = dzu + n;          /* 12n so far incl. M */
-    double* s = dzl + n;            /* p each */
-    double* z = s + p;
-    double* rp = z + p;
-    double* ds = rp + p;
-    double* dz = ds + p;
-    double* dsa = dz + p;
-    double* dza = dsa + p;
-    double* t = dza + p;
-    double* rc = t + p;
-    double* dsua_ = rc + p;         /* box affine directions, n each */
-    double* dzua_ = dsua_ + n;
-    double* dsla_ = dzua_ + n;
-    double* dzla_ = dsla_ + n;
+    const double *lb = P->lb, *ub = P->ub;
+    double *s = W->s, *z = W->z, *rp = W->rp, *rd = W->rd, *du = W->du;
+    double *su = W->su, *sl = W->sl, *zu = W->zu, *zl = W->zl, *rpu = W->rpu, *rpl = W->rpl;
     const int m = p + 2 * nb;
+    double xpol[64];
 
     for (int i = 0; i < n; ++i) {
         double v = 0.0;
@@ -81,60 +232,75 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
         u[i] = v;
     }
     double bnorm = 0.0, qnorm = 0.0;
+    gmul(P, u, W->gv);
     for (int r = 0; r < p; ++r) {
-        double gu = 0.0;
-        for (int j = 0; j < n; ++j) gu += G[r * n + j] * u[j];
-        double sv = w[r] - gu;
+        double sv = w[r] - W->gv[r];
         s[r] = sv > 1.0 ? sv : 1.0;
         z[r] = 1.0;
         if (fabs(w[r]) > bnorm) bnorm = fabs(w[r]);
     }
-    for (int i = 0; i < nb; ++i) {
-        double a = ub[i] - u[i], b = u[i] - lb[i];
-        su[i] = a > 1.0 ? a : 1.0;
-        sl[i] = b > 1.0 ? b : 1.0;
-        zu[i] = zl[i] = 1.0;
-        if (fabs(ub[i]) > bnorm) bnorm = fabs(ub[i]);
-        if (fabs(lb[i]) > bnorm) bnorm = fabs(lb[i]);
+    for (int i = 0; i < n; ++i) {
+        su[i] = sl[i] = 1.0;
+        zu[i] = zl[i] = boxed ? 1.0 : 0.0;
+        if (boxed) {
+            double a = ub[i] - u[i], b = u[i] - lb[i];
+            su[i] = a > 1.0 ? a : 1.0;
+            sl[i] = b > 1.0 ? b : 1.0;
+            if (fabs(ub[i]) > bnorm) bnorm = fabs(ub[i]);
+            if (fabs(lb[i]) > bnorm) bnorm = fabs(lb[i]);
+        }
+        if (fabs(q[i]) > qnorm) qnorm = fabs(q[i]);
     }
-    for (int i = 0; i < n; ++i) if (fabs(q[i]) > qnorm) qnorm = fabs(q[i]);
     bnorm += 1.0; qnorm += 1.0;
 
     int status = 2, it;
     for (it = 0; it < max_iter; ++it) {
-        /* residuals */
-        double rpn = 0.0, rdn = 0.0, mu = 0.0;
+        /* ---- residuals and their scales ---- */
+        double rpn = 0.0, rdn = 0.0, mu = 0.0, gun = 0.0, un = 0.0, hun = 0.0, gzn = 0.0;
+        gmul(P, u, W->gv);
         for (int r = 0; r < p; ++r) {
-            double gu = 0.0;
-            for (int j = 0; j < n; ++j) gu += G[r * n + j] * u[j];
-            rp[r] = gu + s[r] - w[r];
+            if (fabs(W->gv[r]) > gun) gun = fabs(W->gv[r]);
+            rp[r] = W->gv[r] + s[r] - w[r];
             if (fabs(rp[r]) > rpn) rpn = fabs(rp[r]);
             mu += s[r] * z[r];
         }
-        for (int i = 0; i < nb; ++i) {
-            rpu[i] = u[i] + su[i] - ub[i];
-            rpl[i] = -u[i] + sl[i] + lb[i];
+        for (int i = 0; i < n; ++i) {
+            rpu[i] = boxed ? u[i] + su[i] - ub[i] : 0.0;
+            rpl[i] = boxed ? -u[i] + sl[i] + lb[i] : 0.0;
             if (fabs(rpu[i]) > rpn) rpn = fabs(rpu[i]);
             if (fabs(rpl[i]) > rpn) rpn = fabs(rpl[i]);
-            mu += su[i] * zu[i] + sl[i] * zl[i];
+            if (boxed) mu += su[i] * zu[i] + sl[i] * zl[i];
+            if (boxed && fabs(u[i]) > un) un = fabs(u[i]);
         }
         mu /= (m > 0 ? m : 1);
+        gtmul(P, z, W->nv1);                      /* nv1 = G'z (Farkas c) */
         for (int i = 0; i < n; ++i) {
-            double v = q[i];
-            for (int j = 0; j < n; ++j) v += H[i * n + j] * u[j];
-            for (int r = 0; r < p; ++r) v += G[r * n + i] * z[r];
-            if (boxed) v += zu[i] - zl[i];
-            rd[i] = v;
-            if (fabs(v) > rdn) rdn = fabs(v);
+            double hu = 0.0;
+            for (int j = 0; j < n; ++j) hu += P->H[i * n + j] * u[j];
+            double gz = W->nv1[i] + (boxed ? zu[i] - zl[i] : 0.0);
+            rd[i] = q[i] + hu + gz;
+            if (fabs(rd[i]) > rdn) rdn = fabs(rd[i]);
+            if (fabs(hu) > hun) hun = fabs(hu);
+            if (fabs(gz) > gzn) gzn = fabs(gz);
         }
+        double pscale = bnorm, dscale = qnorm;
+        if (1.0 + gun > pscale) pscale = 1.0 + gun;
+        if (1.0 + un > pscale) pscale = 1.0 + un;
+        if (1.0 + hun > dscale) dscale = 1.0 + hun;
+        if (1.0 + gzn > dscale) dscale = 1.0 + gzn;
         if (!isfinite(mu) || !isfinite(rdn)) { status = 3; break; }
-        if (rpn <= tol * bnorm && rdn <= tol * qnorm && mu <= tol_mu) { status = 0; break; }
-        /* Farkas test (rigorous when boxed): min_{box} (G'z)'u > w'z  =>  infeasible */
+        const int res_ok = rpn <= tol * pscale && rdn <= tol * dscale;
+        if (res_ok && mu <= POLISH_MU && polish(P, q, w, W, xpol)) {
+            memcpy(u, xpol, sizeof(double) * n);
+            status = 0;
+            break;
+        }
+        if (res_ok && mu <= tol_mu) { status = 0; break; }
+        /* ---- Farkas test (rigorous when boxed): min_box (G'z)'u > w'z => infeasible ---- */
         if (p > 0) {
             double lo = 0.0, wz = 0.0, scale = 0.0;
             for (int i = 0; i < n; ++i) {
-                double c = 0.0;
-                for (int r = 0; r < p; ++r) c += G[r * n + i] * z[r];
+                double c = W->nv1[i];
                 double bl = boxed ? lb[i] : -UNBOXED_BOUND, bh = boxed ? ub[i] : UNBOXED_BOUND;
                 double a = c * bl, b = c * bh;
                 lo += a < b ? a : b;
@@ -144,81 +310,68 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
             for (int r = 0; r < p; ++r) { wz += w[r] * z[r]; scale += fabs(w[r]) * z[r]; }
             if (lo - wz > 1e-12 * scale) { status = 1; break; }
         }
-        /* M = H + G' diag(z/s) G + diag(box) -- lower triangle only */
-        for (int i = 0; i < n; ++i)
-            for (int j = 0; j <= i; ++j) M[i * n + j] = H[i * n + j];
-        for (int r = 0; r < p; ++r) {
-            double d = z[r] / s[r];
-            const double* g = G + r * n;
-            for (int i = 0; i < n; ++i) {
-                double dg = d * g[i];
-                for (int j = 0; j <= i; ++j) M[i * n + j] += dg * g[j];
-            }
-        }
-        for (int i = 0; i < nb; ++i) M[i * n + i] += zu[i] / su[i] + zl[i] / sl[i];
-        /* guarded right-looking Cholesky, in place (lower) */
-        for (int k = 0; k < n; ++k) {
-            double piv = M[k * n + k];
-            if (!(piv > 0.0)) piv = 1e128;
-            double lkk = sqrt(piv);
-            M[k * n + k] = lkk;
-            double inv = 1.0 / lkk;
-            for (int i = k + 1; i < n; ++i) M[i * n + k] *= inv;
-            for (int j = k + 1; j < n; ++j) {
-                double ljk = M[j * n + k];
-                for (int i = j; i < n; ++i) M[i * n + j] -= M[i * n + k] * ljk;
-            }
-        }
-        /* two solves: predictor (affine) then corrector */
+        /* ---- factor M = H + G' diag(z/s) G + diag(box) ---- */
+        for (int r = 0; r < p; ++r) W->pv1[r] = z[r] / s[r];
+        for (int i = 0; i < n; ++i) W->nv2[i] = boxed ? zu[i] / su[i] + zl[i] / sl[i] : 0.0;
+        factor(P, W->pv1, W->nv2, W->M);
+        /* ---- predictor then corrector (+1 refinement pass on the corrector) ---- */
         double sigma_mu = 0.0;
         for (int pass = 0; pass < 2; ++pass) {
-            double* dS = pass == 0 ? dsa : ds;
-            double* dZ = pass == 0 ? dza : dz;
-            double* dSu = pass == 0 ? dsua_ : dsu;
-            double* dZu = pass == 0 ? dzua_ : dzu;
-            double* dSl = pass == 0 ? dsla_ : dsl;
-            double* dZl = pass == 0 ? dzla_ : dzl;
-            /* rhs = -rd + G' t + box terms, t = (rc - z rp)/s */
+            double* dS = pass == 0 ? W->dsa : W->ds;
+            double* dZ = pass == 0 ? W->dza : W->dz;
+            double* dSu = pass == 0 ? W->dsua : W->dsu;
+            double* dZu = pass == 0 ? W->dzua : W->dzu;
+            double* dSl = pass == 0 ? W->dsla : W->dsl;
+            double* dZl = pass == 0 ? W->dzla : W->dzl;
+            double* rcu = W->nv3; double* rcl = W->nv4;
             for (int r = 0; r < p; ++r) {
-                rc[r] = pass == 0 ? s[r] * z[r] : s[r] * z[r] + dsa[r] * dza[r] - sigma_mu;
-                t[r] = (rc[r] - z[r] * rp[r]) / s[r];
+                W->rc[r] = pass == 0 ? s[r] * z[r] : s[r] * z[r] + W->dsa[r] * W->dza[r] - sigma_mu;
+                W->t[r] = (W->rc[r] - z[r] * rp[r]) / s[r];
             }
+            gtmul(P, W->t, du);
             for (int i = 0; i < n; ++i) {
-                double v = -rd[i];
-                for (int r = 0; r < p; ++r) v += G[r * n + i] * t[r];
+                double v = -rd[i] + du[i];
                 if (boxed) {
-                    double rcu = pass == 0 ? su[i] * zu[i] : su[i] * zu[i] + dsua_[i] * dzua_[i] - sigma_mu;
-                    double rcl = pass == 0 ? sl[i] * zl[i] : sl[i] * zl[i] + dsla_[i] * dzla_[i] - sigma_mu;
-                    v += (rcu - zu[i] * rpu[i]) / su[i] - (rcl - zl[i] * rpl[i]) / sl[i];
-                    /* stash rc for the box dz computation */
-                    dSu[i] = rcu; dSl[i] = rcl;
+                    rcu[i] = pass == 0 ? su[i] * zu[i] : su[i] * zu[i] + W->dsua[i] * W->dzua[i] - sigma_mu;
+                    rcl[i] = pass == 0 ? sl[i] * zl[i] : sl[i] * zl[i] + W->dsla[i] * W->dzla[i] - sigma_mu;
+                    v += (rcu[i] - zu[i] * rpu[i]) / su[i] - (rcl[i] - zl[i] * rpl[i]) / sl[i];
                 }
                 du[i] = v;
             }
-            /* forward: L y = rhs */
-            for (int i = 0; i < n; ++i) {
-                double v = du[i];
-                for (int j = 0; j < i; ++j) v -= M[i * n + j] * du[j];
-                du[i] = v / M[i * n + i];
-            }
-            /* backward: L' x = y */
-            for (int i = n - 1; i >= 0; --i) {
-                double v = du[i];
-                for (int j = i + 1; j < n; ++j) v -= M[j * n + i] * du[j];
-                du[i] = v / M[i * n + i];
-            }
+            chol_solve(W->M, n, du);
+            gmul(P, du, W->gv);
             for (int r = 0; r < p; ++r) {
-                double gd = 0.0;
-                for (int j = 0; j < n; ++j) gd += G[r * n + j] * du[j];
-                dS[r] = -rp[r] - gd;
-                dZ[r] = (-rc[r] - z[r] * dS[r]) / s[r];
+                dS[r] = -rp[r] - W->gv[r];
+                dZ[r] = (-W->rc[r] - z[r] * dS[r]) / s[r];
             }
             for (int i = 0; i < nb; ++i) {
-                double rcu = dSu[i], rcl = dSl[i];
                 dSu[i] = -rpu[i] - du[i];
                 dSl[i] = -rpl[i] + du[i];
-                dZu[i] = (-rcu - zu[i] * dSu[i]) / su[i];
-                dZl[i] = (-rcl - zl[i] * dSl[i]) / sl[i];
+                dZu[i] = (-rcu[i] - zu[i] * dSu[i]) / su[i];
+                dZl[i] = (-rcl[i] - zl[i] * dSl[i]) / sl[i];
+            }
+            if (pass == 1) {
+                /* refinement: e = H du + G'dz + box + rd ; M c = -e ; du += c, ds -= G c, dz += z G c / s */
+                double* e = W->nv5;
+                gtmul(P, dZ, e);
+                for (int i = 0; i < n; ++i) {
+                    double v = e[i] + rd[i] + (boxed ? dZu[i] - dZl[i] : 0.0);
+                    for (int j = 0; j < n; ++j) v += P->H[i * n + j] * du[j];
+                    e[i] = -v;
+                }
+                chol_solve(W->M, n, e);
+                gmul(P, e, W->gv);
+                for (int r = 0; r < p; ++r) {
+                    dS[r] -= W->gv[r];
+                    dZ[r] += z[r] * W->gv[r] / s[r];
+                }
+                for (int i = 0; i < n; ++i) {
+                    du[i] += e[i];
+                    if (boxed) {
+                        dSu[i] -= e[i]; dZu[i] += zu[i] * e[i] / su[i];
+                        dSl[i] += e[i]; dZl[i] -= zl[i] * e[i] / sl[i];
+                    }
+                }
             }
             double amax = INFINITY;
             amax = maxstep(s, dS, p, amax);
@@ -240,25 +393,30 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
                 double a = STEP_FRAC * amax;
                 if (a > 1.0) a = 1.0;
                 for (int i = 0; i < n; ++i) u[i] += a * du[i];
-                for (int r = 0; r < p; ++r) { s[r] += a * ds[r]; z[r] += a * dz[r]; }
+                for (int r = 0; r < p; ++r) { s[r] += a * dS[r]; z[r] += a * dZ[r]; }
                 for (int i = 0; i < nb; ++i) {
-                    su[i] += a * dsu[i]; zu[i] += a * dzu[i];
-                    sl[i] += a * dsl[i]; zl[i] += a * dzl[i];
+                    su[i] += a * dSu[i]; zu[i] += a * dZu[i];
+                    sl[i] += a * dSl[i]; zl[i] += a * dZl[i];
                 }
             }
         }
+    }
+    if (status == 2 && polish(P, q, w, W, xpol)) {   /* last resort at the iteration limit */
+        memcpy(u, xpol, sizeof(double) * n);
+        status = 0;
     }
     *iters_out = it < max_iter ? it : max_iter;
     return status;
 }
 
 /* Batched entry point.  Arrays are row-major fp64.  lb/ub NULL => no input box.
- * xref NULL => goal for every instance.  Returns 0. */
+ * xref NULL => goal for every instance.  Returns 0, or -1 for n > 64. */
 int oracle_solve_batch(int n, int p, int npre, const double* H, const double* G, const double* w0,
                        const double* E, const double* pre_w0, const double* pre_E, const double* hq,
                        const double* lb, const double* ub, const double* goal, int64_t B,
                        const double* x0, const double* xref, double* u_out, int32_t* status,
                        int32_t* iters, double tol, double tol_mu, int max_iter, int nthreads) {
+    if (n > 64) return -1;
     qp_t P = {n, p, lb != NULL && ub != NULL, H, G, lb, ub};
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -267,7 +425,8 @@ int oracle_solve_batch(int n, int p, int npre, const double* H, const double* G,
 #endif
 #pragma omp parallel
     {
-        double* work = (double*)malloc(sizeof(double) * (size_t)(n * n + 17 * n + 9 * p + 1));
+        work_t W;
+        work_alloc(&W, n, p);
         double* q = (double*)malloc(sizeof(double) * (size_t)(n + 1));
         double* w = (double*)malloc(sizeof(double) * (size_t)(p + 1));
 #pragma omp for schedule(dynamic, 16)
@@ -297,10 +456,10 @@ int oracle_solve_batch(int n, int p, int npre, const double* H, const double* G,
                 w[r] = v;
             }
             int it = 0;
-            status[b] = solve_one(&P, q, w, u, work, tol, tol_mu, max_iter, &it);
+            status[b] = solve_one(&P, q, w, u, &W, tol, tol_mu, max_iter, &it);
             iters[b] = it;
         }
-        free(work); free(q); free(w);
+        free(W.M); free(q); free(w);
     }
     return 0;
 }

@@ -31,6 +31,11 @@ TOL_RES = 1e-10
 TOL_MU = 1e-12
 MAX_ITER = 60
 STEP_FRAC = 0.99
+REFINE = 1                 # iterative-refinement passes on the corrector direction
+POLISH_MU = 1e-8           # attempt the active-set polish once mu <= POLISH_MU (and residuals ok)
+POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
+POLISH_REFINE = 3          # iterative-refinement passes of the polish
+POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
 UNBOXED_BOUND = 1e9        # |u_i| bound assumed by the Farkas test for unboxed variables
 PRE_TOL = 1e-9             # zero-row precondition tolerance
 ZERO_ROW = 1e-12           # rows with ||G_r||_2 <= ZERO_ROW * max_r ||G_r||_2 are x0-only rows
@@ -48,7 +53,7 @@ def normalize_rows(G, w0, E):
 
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
-        trace=None):
+        trace=None, refine=REFINE, polish=True, info=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -89,11 +94,21 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         rpn = max(np.abs(rp).max() if p else 0.0, np.abs(rpu).max() if nb else 0.0,
                   np.abs(rpl).max() if nb else 0.0)
         rdn = np.abs(rd).max()
+        # tolerances scale with the magnitude of the terms each residual sums (roundoff floor)
+        Hu = H @ u; Gtz = G.T @ z
+        pscale = max(bnorm, 1.0 + (np.abs(Gu).max() if p else 0.0), 1.0 + (np.abs(u).max() if nb else 0.0))
+        dscale = max(qnorm, 1.0 + np.abs(Hu).max(), 1.0 + np.abs(Gtz + box_T(zu, zl)).max())
         if trace is not None:
             trace.append((it, mu, rpn, rdn))
         if not np.isfinite(mu) or not np.isfinite(rdn):
             return u, STATUS_NUMERICAL, it, z
-        if rpn <= tol * bnorm and rdn <= tol * qnorm and mu <= tol_mu:
+        if polish and rpn <= tol * pscale and rdn <= tol * dscale and mu <= POLISH_MU:
+            up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl)
+            if info is not None:
+                info.setdefault("polish", []).append((it, ok))
+            if ok:
+                return up, STATUS_OPTIMAL, it, z
+        if rpn <= tol * pscale and rdn <= tol * dscale and mu <= tol_mu:
             return u, STATUS_OPTIMAL, it, z
         # Farkas test: for every u in the box, (G'z)'u >= lo; if lo > w'z then no u
         # satisfies G u <= w (z >= 0).  Rigorous when all variables are boxed.
@@ -133,11 +148,72 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         smu = sigma * mu
         du, ds, dz, dsu, dzu, dsl, dzl = solve(s * z + ds * dz - smu, su * zu + dsu * dzu - smu,
                                                sl * zl + dsl * dzl - smu)
+        for _ in range(refine):
+            # residual of the dual equation H du + A'dz = -rd for the reconstructed direction;
+            # correct with the same factor: M dU = -e, dS = -A dU, dZ = -z dS / s
+            e = H @ du + G.T @ dz + rd + (box_T(dzu, dzl) if boxed else 0.0)
+            cu = _chol_solve(Lc, -e)
+            cs = -(G @ cu)
+            du = du + cu; ds = ds + cs; dz = dz - z * cs / s
+            if boxed:
+                dsu = dsu - cu; dzu = dzu + zu * cu / su
+                dsl = dsl + cu; dzl = dzl - zl * cu / sl
         a = min(1.0, STEP_FRAC * min(_maxstep(s, ds), _maxstep(z, dz), _maxstep(su, dsu),
                                      _maxstep(zu, dzu), _maxstep(sl, dsl), _maxstep(zl, dzl)))
         u = u + a * du; s = s + a * ds; z = z + a * dz
         su = su + a * dsu; zu = zu + a * dzu; sl = sl + a * dsl; zl = zl + a * dzl
+    if polish:
+        up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl)
+        if ok:
+            return up, STATUS_OPTIMAL, max_iter, z
     return u, STATUS_MAXITER, max_iter, z
+
+
+def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE):
+    """Active-set polish.  Active set from the IPM iterate (s < z); solve the
+    equality-constrained KKT [[H, A'], [A, 0]] [x; y] = [-q; b_act] by iterative refinement on
+    the regularised factor  H + A'A/delta  (the IPM's M with d = 1/delta on active rows, 0 else);
+    accept only if x is primal feasible and the active multipliers are nonnegative."""
+    n = len(q)
+    boxed = lb is not None
+    dg = np.where(s < z, 1.0 / delta, 0.0)
+    M = H + (G.T * dg) @ G
+    if boxed:
+        du_ = np.where(su < zu, 1.0 / delta, 0.0); dl_ = np.where(sl < zl, 1.0 / delta, 0.0)
+        M[np.diag_indices(n)] += du_ + dl_
+    else:
+        du_ = dl_ = np.zeros(n)
+    L = _chol_guarded(M)
+    ag = dg > 0; au = du_ > 0; al = dl_ > 0
+    bg = np.where(ag, w, 0.0)
+    bu = np.where(au, ub, 0.0) if boxed else np.zeros(n)
+    bl = np.where(al, lb, 0.0) if boxed else np.zeros(n)
+
+    def At(yg, yu, yl):
+        return G.T @ yg + yu - yl
+
+    def ksolve(rx, ryg, ryu, ryl):
+        # [[H, A'], [A, -delta I]] on the active rows: dy = (A dx - ry)/delta
+        dx = _chol_solve(L, rx + At(dg * ryg, du_ * ryu, dl_ * ryl))
+        return dx, dg * (G @ dx - ryg), du_ * (dx - ryu), dl_ * (-dx - ryl)
+
+    x, yg, yu, yl = ksolve(-q, bg, bu, -bl)
+    for _ in range(refine):
+        rx = -q - H @ x - At(yg, yu, yl)
+        ryg = np.where(ag, bg - G @ x, 0.0)
+        ryu = np.where(au, bu - x, 0.0)
+        ryl = np.where(al, -bl + x, 0.0)
+        dx, dyg, dyu, dyl = ksolve(rx, ryg, ryu, ryl)
+        x = x + dx; yg = yg + dyg; yu = yu + dyu; yl = yl + dyl
+    wscale = 1.0 + max(np.abs(w).max() if len(w) else 0.0, np.abs(ub).max() if boxed else 0.0,
+                       np.abs(lb).max() if boxed else 0.0)
+    viol = max((G @ x - w).max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
+               (lb - x).max() if boxed else -np.inf)
+    ymin = min(yg.min() if len(yg) else 0.0, yu.min() if boxed else 0.0, yl.min() if boxed else 0.0)
+    yscale = 1.0 + max(np.abs(yg).max() if len(yg) else 0.0, np.abs(yu).max() if boxed else 0.0,
+                       np.abs(yl).max() if boxed else 0.0)
+    ok = bool(viol <= POLISH_TOL * wscale and ymin >= -POLISH_TOL * yscale and np.all(np.isfinite(x)))
+    return x, ok
 
 
 def _maxstep(v, dv):
@@ -214,7 +290,7 @@ def lp_margin(G, w, lb, ub, cap=1.0):
     return float(r.x[-1])
 
 
-def solve_instance(asm, x0, xref=None, **kw):
+def solve_instance(asm, x0, xref=None, info=None, **kw):
     """Full per-step oracle for one instance of an ``assembly.Assembly``:
     preconditions on x0-only rows, normalised IPM, certificate.
     Returns dict(status, iters, u, u_exact, certified, margin)."""
@@ -229,7 +305,7 @@ def solve_instance(asm, x0, xref=None, **kw):
         out.update(status=STATUS_INFEASIBLE, iters=0, u=np.zeros(len(q)), u_exact=None,
                    certified=False, margin=float(pre.min()))
         return out
-    u, st, it, _ = ipm(asm.H, q, Gn, wn, asm.lb, asm.ub, **kw)
+    u, st, it, _ = ipm(asm.H, q, Gn, wn, asm.lb, asm.ub, info=info, **kw)
     out.update(status=st, iters=it, u=u)
     if st == STATUS_OPTIMAL:
         ue, ok, res = certify(asm.H, q, Gn, wn, asm.lb, asm.ub, u)
