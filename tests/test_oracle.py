@@ -1,0 +1,145 @@
+"""The oracle against the golden vectors produced from the reference (CPU only).
+
+Pins (see tests/golden/meta.json, tools/make_golden.py):
+  * assembly (T, S, H, h) == outputs of the reference's lib/matrix_gen.py;
+  * environments / configuration == the reference's objects and constants;
+  * terminal-set data == the reference's terminal_sets/*.npy;
+  * plant == the reference's lib/simulator.CarSimulator on seeded pairs;
+  * QP solutions: KKT-certified optimum (parity vs cvxpy itself is unpinned: absent).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CONFIGS, GOLDEN, REPO, TERMINAL_SETS
+
+from oracle import assembly as oa
+from oracle import qp as oq
+
+
+def _meta():
+    with open(os.path.join(GOLDEN, "meta.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_assembly_matches_reference_matrix_gen(name, N):
+    g = np.load(os.path.join(GOLDEN, f"assembly_{name}_N{N}.npz"))
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+    np.testing.assert_array_equal(asm.A, g["A"])
+    np.testing.assert_array_equal(asm.B, g["B"])
+    np.testing.assert_allclose(asm.T, g["T"], rtol=0, atol=1e-14)   # BLAS rounding only
+    np.testing.assert_allclose(asm.S, g["S"], rtol=0, atol=1e-14)
+    np.testing.assert_allclose(asm.H, g["H"], rtol=1e-14, atol=1e-11)
+    np.testing.assert_allclose(asm.h, g["h"], rtol=1e-14, atol=1e-11)
+    np.testing.assert_array_equal(asm.term_A[:, -4:], g["term"][:, :4])
+    np.testing.assert_array_equal(asm.term_b, g["term"][:, 4])
+    # DARE fixed point (mpc.py:70) and LQR gain (mpc.py:81)
+    A, B, P, Q, R = asm.A, asm.B, asm.P, oa.STAGE_COST_Q, oa.STAGE_COST_R
+    res = A.T @ P @ A - P - A.T @ P @ B @ np.linalg.solve(R + B.T @ P @ B, B.T @ P @ A) + Q
+    assert np.abs(res).max() < 1e-9
+    np.testing.assert_allclose(asm.K, g["K"], rtol=1e-12)
+    # survey §8a a3 spot values
+    assert abs(P[0, 0] - 60.13) < 5e-3 and abs(P[2, 2] - 843.30) < 5e-3
+
+
+def test_environment_and_configuration_data():
+    meta = _meta()
+    for name, (rows, rhs, goal) in oa.ENVIRONMENTS.items():
+        e = meta["environments"][name]
+        np.testing.assert_array_equal(np.asarray(rows, float), np.asarray(e["constraints_A"]))
+        np.testing.assert_array_equal(np.asarray(rhs, float), np.asarray(e["constraints_b"]))
+        assert list(goal) == e["goal"]
+    c = meta["configuration"]
+    assert c["DT_CONTROL"] == oa.DT_CONTROL and c["N"] == oa.N_HORIZON
+    assert c["LINEARIZE_STATE"] == oa.LINEARIZE_STATE and c["LINEARIZE_INPUT"] == oa.LINEARIZE_INPUT
+    np.testing.assert_array_equal(np.asarray(c["Q"]), oa.STAGE_COST_Q)
+    np.testing.assert_array_equal(np.asarray(c["R"]), oa.STAGE_COST_R)
+
+
+def test_terminal_set_files_are_reference_copies():
+    # byte-identical copies of the reference data (md5 recorded in DESIGN.md)
+    import hashlib
+    want = {"RoadEnv_30_1.5_0_0.npy": "b8e85fd87a9d03968feeb45884bce20f",
+            "RoadMultipleCarsEnv_30_1.5_0_0.npy": "e51cd11d0a547780b53b624cc09eeacf",
+            "RoadOneCarEnv_29.9_-1.5_0_0.npy": "19e967d9a5804a3ed5251c0699e112e6"}
+    for f, h in want.items():
+        with open(os.path.join(TERMINAL_SETS, f), "rb") as fh:
+            assert hashlib.md5(fh.read()).hexdigest() == h
+    assert oa.terminal_set_filename("RoadOneCarEnv", [29.9, -1.5, 0, 0]) == "RoadOneCarEnv_29.9_-1.5_0_0.npy"
+
+
+def test_terminal_fallback_box(tmp_path):
+    asm = oa.build("RoadEnv", 10, terminal_set_dir=str(tmp_path))
+    assert asm.term_file is None and asm.term_A.shape == (8, 44)
+    np.testing.assert_array_equal(asm.term_A[:4, -4:], np.diag([1, 1, 1, 0]))
+    np.testing.assert_array_equal(asm.term_b, np.hstack((asm.goal, -asm.goal)))
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_numpy_ipm_against_golden(name, N):
+    g = np.load(os.path.join(GOLDEN, f"qp_{name}_N{N}.npz"))
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+    for i in range(0, 64, 4):
+        r = oq.solve_instance(asm, g["x0"][i])
+        assert r["status"] == g["status"][i]
+        assert r["iters"] == g["iters"][i]
+        if r["status"] == 0:
+            assert np.abs(r["u"] - g["u_star"][i]).max() <= 1e-8
+        assert (g["margin"][i] >= 0) == (g["status"][i] == 0)
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_c_oracle_against_golden(name, N):
+    from oracle.cpu import CpuProblem
+    g = np.load(os.path.join(GOLDEN, f"qp_{name}_N{N}.npz"))
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+    u, st, it = CpuProblem(asm).solve(g["x0"], threads=2)
+    np.testing.assert_array_equal(st, g["status"])
+    np.testing.assert_array_equal(it, g["iters"])
+    ok = st == 0
+    assert np.abs(u[ok] - g["u_star"][ok]).max() <= 1e-8
+
+
+def test_c_oracle_status_against_lp_ground_truth():
+    """Box-Farkas infeasibility certificates and optimal statuses agree with HiGHS."""
+    from oracle.cpu import CpuProblem
+    asm = oa.build("RoadOneCarEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    rng = np.random.default_rng(123)
+    B = 400
+    X = np.stack([rng.uniform(4.9, 29.9, B), rng.uniform(-3, 3, B), rng.uniform(-np.pi / 8, np.pi / 8, B),
+                  rng.uniform(-1, 5, B)], axis=1)
+    u, st, it = CpuProblem(asm).solve(X, threads=2)
+    Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
+    for i in range(B):
+        pre = pw - pE @ X[i]
+        if pre.size and pre.min() < -oq.PRE_TOL:
+            assert st[i] == 1
+            continue
+        m = oq.lp_margin(Gn, w0n - En @ X[i], asm.lb, asm.ub)
+        if abs(m) > 1e-7:
+            assert (st[i] == 0) == (m > 0), (i, st[i], m)
+    assert (st == 2).sum() == 0
+
+
+def test_plant_restatement_matches_reference_simulator():
+    g = np.load(os.path.join(GOLDEN, "plant.npz"))
+    for s, u, nxt in zip(g["state"], g["u"], g["next"]):
+        np.testing.assert_allclose(oa.plant_step(s, u), nxt, rtol=0, atol=1e-14)
+
+
+def test_closed_loop_statefb_reproduces_golden_trace():
+    """examples/run_MPCStateFB.py loop (RoadMultipleCarsEnv, N=20, start [5,-1.5,0.1,0]) with the
+    oracle QP reaches the goal tolerance in 52 steps, as recorded from the reference plant."""
+    g = np.load(os.path.join(GOLDEN, "closed_loop_statefb.npz"))
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    state, u = np.array([5, -1.5, 0.1, 0.0]), np.zeros(2)
+    for i in range(len(g["states"])):
+        state = oa.plant_step(state, u)
+        np.testing.assert_allclose(state, g["states"][i], atol=1e-7)
+        r = oq.solve_instance(asm, state)
+        assert r["status"] == 0
+        u = r["u_exact"][:2] if r["certified"] else r["u"][:2]
+    assert np.all(np.abs(state - asm.goal) <= 1e-1)
