@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=24576)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 3 dense 1-wave/SIMD)")
+    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 3 dense 1-wave/SIMD)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -104,35 +104,49 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    from carmpc_amd.qp import SolverSettings, solve_segments
+    from carmpc_amd.qp import SolverSettings
     settings = SolverSettings(kernel=args.kernel)
     ctrls = build_problems(device)
     probs = [c.qp for c in ctrls]
     goals = [c.goal for c in ctrls]
     X, env, offsets = sample_shard(rank, args.per_gpu, goals)
     Xd = torch.as_tensor(X).to(device)
+    B = args.per_gpu
+    u = torch.zeros((B, 40), dtype=torch.float64, device=device)
+    st = torch.empty(B, dtype=torch.int32, device=device)
+    it = torch.empty(B, dtype=torch.int32, device=device)
+    segs = [(probs[j], slice(int(offsets[j]), int(offsets[j + 1]))) for j in range(len(ENVS))]
+    kernels = [settings.kernel or p.kernel for p in probs]
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
+
+    def step(events=None):
+        # one pass of the hot path: every segment's solve launch on one stream
+        for j, (p, sl) in enumerate(segs):
+            if events is not None:
+                events[j].record(stream)
+            p.solve(Xd[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
+        if events is not None:
+            events[len(segs)].record(stream)
+
     for _ in range(args.warmup):
-        u, st, it = solve_segments(probs, offsets, Xd, settings=settings, stream=stream)
+        step()
     torch.cuda.synchronize()
 
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(segs) + 1)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev0[k].record(stream)
-        u, st, it = solve_segments(probs, offsets, Xd, settings=settings, stream=stream)
-        ev1[k].record(stream)
+        step(evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev0, ev1)]))
+    seg_ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(len(segs))] for e in evs]).mean(axis=0)
+    kern_ms = float(seg_ms.sum())
     t = torch.tensor([wall], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -143,28 +157,34 @@ def main():
     torch.cuda.synchronize()
     te = time.perf_counter()
     Xe = Xh.to(device, non_blocking=True)
-    ue, se, _ = solve_segments(probs, offsets, Xe, settings=settings, stream=stream)
-    uh = ue.to("cpu"); sh = se.to("cpu")
+    for p, sl in segs:
+        p.solve(Xe[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
+    uh = u.to("cpu"); sh = st.to("cpu")
     torch.cuda.synchronize()
-    e2e = args.per_gpu / (time.perf_counter() - te)
+    e2e = B / (time.perf_counter() - te)
 
     st_np = st.cpu().numpy(); it_np = it.cpu().numpy()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
-    total = args.per_gpu * world * args.steps
+    total = B * world * args.steps
     value = total / wall_max
     status_split = {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
                                                                       "numerical"))}
+    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave"}
+    kdesc = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
+             2: "ipm_staged (wavefront per QP, stage-structured G/H products and Riccati-style M build)",
+             3: "ipm_dense, 4 waves per workgroup"}
+    used = sorted(set(kernels))
     out = {
         "metric": "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X",
         "value": round(value, 1), "unit": "QP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded config-5 state distribution)",
-        "config": {"workload": "config5_mixed_road_envs_N20_weak", "per_gpu_batch": args.per_gpu,
-                   "global_batch": args.per_gpu * world, "envs": list(ENVS), "N": N_HOR, "n": 40,
-                   "p_qp_rows": [p.p for p in probs], "kernel": "ipm_dense (wavefront per QP, G/H in LDS)",
+        "config": {"workload": "config5_mixed_road_envs_N20_weak", "per_gpu_batch": B,
+                   "global_batch": B * world, "envs": list(ENVS), "N": N_HOR, "n": 40,
+                   "p_qp_rows": [p.p for p in probs], "kernel": "; ".join(kdesc[k] for k in used),
                    "parallelism": f"shard{world} (no data-path collective)"},
         "status_split": status_split,
         "gpu_iters_mean": float(it_np[st_np == 0].mean()),
@@ -172,31 +192,46 @@ def main():
     }
     # roofline: canonical FP64 flops with I_ref from the oracle on a sample of this batch
     seg = np.diff(offsets)
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         thr = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         cpu_qps, ncpu, iref = cpu_baseline(ctrls, X, env, offsets, args.cpu_sample, thr)
         out["cpu_baseline"] = {"value": round(cpu_qps, 1), "unit": "QP/s", "cores": thr, "kind": "port",
                                "sample": f"{ncpu} instances of this shard (equal per env), oracle/ipm.c "
                                          f"OpenMP x{thr}, {platform.processor() or platform.machine()}"}
         I_ref = {k: v[1] for k, v in iref.items()}
+        iref_src = "oracle/ipm.c on the cpu_baseline sample"
     else:
         I_ref = {ENVS[j]: float(it_np[offsets[j]:offsets[j + 1]].mean()) for j in range(len(ENVS))}
-    flops_step = sum(seg[j] * I_ref[ENVS[j]] * probs[j].canonical_flops_per_iter() for j in range(len(ENVS)))
+        iref_src = "GPU iteration counts of this batch"
+    canon = [seg[j] * I_ref[ENVS[j]] * probs[j].canonical_flops_per_iter() for j in range(len(ENVS))]
+    execd = [float(it_np[offsets[j]:offsets[j + 1]].sum()) * probs[j].executed_flops_per_iter(kernels[j])
+             for j in range(len(ENVS))]
+    flops_step = float(sum(canon))
     achieved = flops_step / (kern_ms * 1e-3) / 1e12
-    bytes_step = args.per_gpu * (32 + 4 + 8 * 40 + 4 + 4)     # x0 + env in; u + status + iters out
+    bytes_step = B * (32 + 4 + 8 * 40 + 4 + 4)     # x0 + env in; u + status + iters out
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            traffic = tj.get("hbm_bytes_per_step")
+            key = "+".join(kname[k] for k in used)
+            ent = tj.get(key)
+            if ent is not None and ent.get("per_gpu_batch") == B:
+                traffic = ent.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
+    launches = [{"env": ENVS[j], "kernel": kname[kernels[j]], "instances": int(seg[j]), "ms": round(float(seg_ms[j]), 4),
+                 "canonical_TFLOPs": round(canon[j] / (seg_ms[j] * 1e-3) / 1e12, 4),
+                 "executed_TFLOPs": round(execd[j] / (seg_ms[j] * 1e-3) / 1e12, 4)} for j in range(len(ENVS))]
     out["roofline"] = {"bound": "mfma", "compute": "fp64 FMA (vector; FP64 vector peak == FP64 matrix peak)",
                        "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                        "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": traffic,
+                       "flops": "canonical dense-IPM count (SURVEY §8d) x I_ref",
                        "kernel_ms_per_step": round(kern_ms, 4), "canonical_flops_per_step": flops_step,
-                       "I_ref": I_ref, "algorithmic_hbm_GBps": round(bytes_step / (kern_ms * 1e-3) / 1e9, 3)}
+                       "executed_flops_per_step": float(sum(execd)),
+                       "executed_TFLOPs": round(sum(execd) / (kern_ms * 1e-3) / 1e12, 4),
+                       "I_ref": I_ref, "I_ref_source": iref_src, "launches": launches,
+                       "algorithmic_hbm_GBps": round(bytes_step / (kern_ms * 1e-3) / 1e9, 3)}
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -21,7 +21,8 @@ STATUS_NAMES = {OPTIMAL: "optimal", PRIMAL_INFEASIBLE: "primal_infeasible", MAX_
 EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_problem_destroy",
            "carmpc_problem_info", "carmpc_problem_get", "carmpc_solve_batch", "carmpc_solve_segments",
            "carmpc_observer_batch", "carmpc_plant_step_batch", "carmpc_canonical_flops_per_iter",
-           "carmpc_last_error", "carmpc_version")
+           "carmpc_last_error", "carmpc_version", "carmpc_problem_kernel",
+           "carmpc_executed_flops_per_iter")
 
 
 class CarMPCNativeError(RuntimeError):
@@ -73,6 +74,8 @@ def load():
         "carmpc_canonical_flops_per_iter": ([i32, i32], ctypes.c_double),
         "carmpc_last_error": ([], ctypes.c_char_p),
         "carmpc_version": ([], ctypes.c_char_p),
+        "carmpc_problem_kernel": ([vp], ctypes.c_int),
+        "carmpc_executed_flops_per_iter": ([vp, i32], ctypes.c_double),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -111,12 +111,175 @@ int finish_padded(carmpc_problem* P, const double* H, const double* hq, const do
     P->dev.boxed = (lb && ub) ? 1 : 0;
     return CARMPC_OK;
 }
+
+// Opposite-row pairs of the packed rows (oracle/qp.py::opposite_pairs): row r' with
+// G_r' = -G_r, w0_r' = -w0_r, E_r' = -E_r exactly.  G is p x ldg (first n columns used).
+std::vector<int32_t> find_pairs(const std::vector<double>& G, int p, int ldg, int n, const std::vector<double>& w0,
+                                const std::vector<double>& E, int* npairs) {
+    std::vector<int32_t> partner(p, -1);
+    *npairs = 0;
+    for (int r = 0; r < p; ++r) {
+        for (int r2 = 0; r2 < p && partner[r] < 0; ++r2) {
+            if (r2 == r || w0[r2] != -w0[r]) continue;
+            bool same = true;
+            for (int k = 0; k < NX && same; ++k) same = E[(size_t)r2 * NX + k] == -E[(size_t)r * NX + k];
+            for (int j = 0; j < n && same; ++j) same = G[(size_t)r2 * ldg + j] == -G[(size_t)r * ldg + j];
+            if (same) {
+                partner[r] = r2;
+                ++*npairs;
+            }
+        }
+    }
+    return partner;
+}
+
+// Download the packed rows, find opposite pairs, upload D.partner (left null when none).
+int setup_pairs(carmpc_problem* P, std::vector<int32_t>& partner) {
+    DevProblem& D = P->dev;
+    partner.assign(D.p, -1);
+    if (D.p == 0) return CARMPC_OK;
+    std::vector<double> G((size_t)D.p * D.ldg), w0(D.p), E((size_t)D.p * NX);
+    HIP_TRY(hipMemcpy(G.data(), D.G, sizeof(double) * G.size(), hipMemcpyDeviceToHost), "readback G");
+    HIP_TRY(hipMemcpy(w0.data(), D.w0, sizeof(double) * w0.size(), hipMemcpyDeviceToHost), "readback w0");
+    HIP_TRY(hipMemcpy(E.data(), D.E, sizeof(double) * E.size(), hipMemcpyDeviceToHost), "readback E");
+    int np = 0;
+    partner = find_pairs(G, D.p, D.ldg, D.n, w0, E, &np);
+    if (np > 0) {
+        int32_t* dp = nullptr;
+        HIP_TRY(upload(P, &dp, partner.data(), partner.size()), "upload partner");
+        D.partner = dp;
+    }
+    return CARMPC_OK;
+}
+
+// Row layout of the staged kernel (ipm_staged.hip): a lane's row slots all act on one
+// predicted state.  State row j of stage k -> lane (k-1) + 32*(j%2), slot j/2; terminal
+// row t (stage N) -> the t-th "tail" lane (L%32 >= N) round-robin, slot t / #tail.
+// qp[r] is the assembled index of packed row r (terminal rows first, then N rows per
+// state row j: mpc.py:196-253).  Returns false when the problem does not fit.
+int stage_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vector<int32_t>& qp, const double* Phi_dev,
+                 const std::vector<int32_t>& partner, bool* ok) {
+    *ok = false;
+    DevProblem& D = P->dev;
+    const int N = D.N, nt = d->n_term_rows;
+    if (D.nu != 2 || !staged_supported_N(N) || D.n != D.nv) return CARMPC_OK;
+    std::vector<int> tail;
+    for (int L = 0; L < 64; ++L)
+        if ((L & 31) >= N) tail.push_back(L);
+    if (nt > 0 && tail.empty()) return CARMPC_OK;
+    std::vector<int> lane_of(D.p), slot_of(D.p);
+    int rs = 1;
+    for (int r = 0; r < D.p; ++r) {
+        const int e = qp[r];
+        if (e < nt) {
+            lane_of[r] = tail[e % tail.size()];
+            slot_of[r] = e / (int)tail.size();
+        } else {
+            const int j = (e - nt) / N, k = (e - nt) % N + 1;
+            lane_of[r] = (k - 1) + 32 * (j % 2);
+            slot_of[r] = j / 2;
+        }
+        rs = std::max(rs, slot_of[r] + 1);
+    }
+    if (rs > kStagedMaxRS) return CARMPC_OK;
+    // packed rows (normalised on the device) back to the host
+    std::vector<double> coefp((size_t)D.p * NX), w0p(D.p), Ep((size_t)D.p * NX), phi((size_t)N * NX * 2);
+    if (D.p > 0) {
+        HIP_TRY(hipMemcpy(coefp.data(), D.row_coef, sizeof(double) * coefp.size(), hipMemcpyDeviceToHost), "readback coef");
+        HIP_TRY(hipMemcpy(w0p.data(), D.w0, sizeof(double) * w0p.size(), hipMemcpyDeviceToHost), "readback w0");
+        HIP_TRY(hipMemcpy(Ep.data(), D.E, sizeof(double) * Ep.size(), hipMemcpyDeviceToHost), "readback E");
+    }
+    HIP_TRY(hipMemcpy(phi.data(), Phi_dev, sizeof(double) * phi.size(), hipMemcpyDeviceToHost), "readback Phi");
+    const size_t ns = (size_t)rs * 64;
+    std::vector<double> sc(ns * NX, 0.0), sw(ns, 0.0), sE(ns * NX, 0.0);
+    std::vector<int32_t> sv(ns, 0), spart(ns, -1);
+    for (int r = 0; r < D.p; ++r) {
+        const size_t e = (size_t)slot_of[r] * 64 + lane_of[r];
+        if (sv[e]) return fail(CARMPC_EINVAL, "stage layout collision");
+        sv[e] = 1;
+        if (partner[r] >= 0) spart[e] = slot_of[partner[r]] * 64 + lane_of[partner[r]];
+        sw[e] = w0p[r];
+        for (int a = 0; a < NX; ++a) { sc[e * NX + a] = coefp[(size_t)r * NX + a]; sE[e * NX + a] = Ep[(size_t)r * NX + a]; }
+    }
+    std::vector<double> pac((size_t)(N + 1) * 8, 0.0), pca((size_t)(N + 1) * 8, 0.0);
+    for (int m = 0; m < N; ++m)
+        for (int a = 0; a < NX; ++a)
+            for (int c = 0; c < 2; ++c) {
+                const double v = phi[((size_t)m * NX + a) * 2 + c];
+                pac[(size_t)(m + 1) * 8 + a * 2 + c] = v;
+                pca[(size_t)(m + 1) * 8 + c * 4 + a] = v;
+            }
+    std::vector<double> mats(60);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            mats[i * 4 + j] = 0.5 * (d->Q[i * 4 + j] + d->Q[j * 4 + i]);
+            mats[16 + i * 4 + j] = 0.5 * (d->P[i * 4 + j] + d->P[j * 4 + i]);
+            mats[32 + i * 4 + j] = d->A[i * 4 + j];
+        }
+    for (int i = 0; i < 8; ++i) mats[48 + i] = d->B[i];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) mats[56 + i * 2 + j] = 0.5 * (d->R[i * 2 + j] + d->R[j * 2 + i]);
+    double *dsc, *dsw, *dsE, *dpac, *dpca, *dmats;
+    int32_t* dsv;
+    HIP_TRY(upload(P, &dsc, sc.data(), sc.size()), "upload s_coef");
+    HIP_TRY(upload(P, &dsw, sw.data(), sw.size()), "upload s_w0");
+    HIP_TRY(upload(P, &dsE, sE.data(), sE.size()), "upload s_E");
+    HIP_TRY(upload(P, &dsv, sv.data(), sv.size()), "upload s_valid");
+    HIP_TRY(upload(P, &dpac, pac.data(), pac.size()), "upload phi_ac");
+    HIP_TRY(upload(P, &dpca, pca.data(), pca.size()), "upload phi_ca");
+    HIP_TRY(upload(P, &dmats, mats.data(), mats.size()), "upload mats");
+    D.s_coef = dsc; D.s_w0 = dsw; D.s_E = dsE; D.s_valid = dsv; D.phi_ac = dpac; D.phi_ca = dpca; D.s_mats = dmats;
+    if (D.partner) {
+        int32_t* dsp = nullptr;
+        HIP_TRY(upload(P, &dsp, spart.data(), spart.size()), "upload s_partner");
+        D.s_partner = dsp;
+    }
+    D.srs = rs;
+    D.staged = 1;
+    *ok = true;
+    return CARMPC_OK;
+}
+
+// Kernel choice for one launch (settings.kernel).
+hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, const double* xref, double* u_out,
+                        int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
+                        int* unsupported) {
+    const bool staged = s.kernel == 2 || s.kernel == 4 || (s.kernel == 0 && D.staged);
+    if (staged) return launch_staged(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    return launch_dense(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+}
 }  // namespace
 
 extern "C" {
 
 const char* carmpc_last_error(void) { return g_err.c_str(); }
-const char* carmpc_version(void) { return "carmpc-mi355x 0.1 (gfx950, dense IPM v1)"; }
+const char* carmpc_version(void) { return "carmpc-mi355x 0.2 (gfx950, dense + staged IPM)"; }
+
+int carmpc_problem_kernel(const carmpc_problem* P) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    return P->dev.staged ? 2 : 1;
+}
+
+// Flops one IPM iteration (predictor + corrector + one refinement) of the given kernel
+// actually performs (multiply-add = 2), DESIGN.md §5.  Masked/padded lanes not counted.
+double carmpc_executed_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
+    if (!P) return 0.0;
+    const double n = P->dev.n, p = P->dev.p, N = P->dev.N;
+    const bool staged = kernel == 2 || kernel == 4 || (kernel == 0 && P->dev.staged);
+    const double chol = n * n * n / 3.0, trisolve = 2.0 * n * n;
+    if (!staged) {
+        const double gv = 2.0 * p * n, hv = 2.0 * n * n;
+        // M build, Cholesky, residual (Gu, Hu, G'z), 3 x (G't, solve, G dx), refinement H du + G'dZ
+        return p * n * n + chol + (gv + hv + gv) + 3.0 * (gv + trisolve + gv) + (hv + gv);
+    }
+    const double pred = 8.0 * N * (N + 1), adj = 8.0 * N * (N + 1);   // Y = S v ; S' lam
+    const double rows = 8.0 * p;                                     // c_r . Y / lam scatter
+    const double qy = 32.0 * N;                                      // Qbar_k Y_k
+    const double mbuild = 24.0 * p + 640.0 * (N - 1) + 64.0 * N + 32.0 * n * N;
+    const double resid = pred + rows + 4.0 * n + rows + qy + 2.0 * adj;
+    const double solve = rows + adj + trisolve + pred + rows;
+    return mbuild + chol + resid + 3.0 * solve + (qy + 4.0 * n);
+}
 
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p) {
     const double N_ = n, P_ = p;
@@ -227,6 +390,10 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     }
     int rc = finish_padded(P, Hh.data(), hh.data(), d->u_lower ? lbv.data() : nullptr, d->u_lower ? ubv.data() : nullptr,
                        d->goal);
+    bool staged = false;
+    std::vector<int32_t> partner;
+    if (rc == CARMPC_OK) rc = setup_pairs(P, partner);
+    if (rc == CARMPC_OK) rc = stage_layout(P, d, qp, Phi, partner, &staged);
     if (rc != CARMPC_OK) {
         delete P;
         return rc;
@@ -283,6 +450,8 @@ int carmpc_problem_create_dense(int32_t n, int32_t p, int32_t nx, const double* 
     }
     D.G = dG; D.w0 = dw0; D.E = dE; D.pre_w0 = dprew; D.pre_E = dpreE;
     int rc = finish_padded(P, H, hq, lb, ub, goal);
+    std::vector<int32_t> partner;
+    if (rc == CARMPC_OK) rc = setup_pairs(P, partner);
     if (rc != CARMPC_OK) {
         delete P;
         return rc;
@@ -327,7 +496,7 @@ int carmpc_solve_batch(const carmpc_problem* P, int64_t batch, const double* x0,
     if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
     const Settings s = make_settings(settings);
     int unsupported = 0;
-    hipError_t e = launch_dense(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
+    hipError_t e = launch_solve(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
     if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
     if (e != hipSuccess) return hipfail(e, "solve launch");
     return CARMPC_OK;
@@ -346,7 +515,7 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
         if (!P) return fail(CARMPC_EINVAL, "null problem in segment list");
         if (ld_u < P->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
         int unsupported = 0;
-        hipError_t e = launch_dense(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
+        hipError_t e = launch_solve(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
                                     ld_u, status + b0, iters ? iters + b0 : nullptr, s, stream, &unsupported);
         if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
         if (e != hipSuccess) return hipfail(e, "segment launch");

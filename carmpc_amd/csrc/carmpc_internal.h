@@ -40,12 +40,26 @@ struct DevProblem {
     const int32_t* row_stage; // p
     const double* row_coef;   // p x NX (normalised with the row)
     const double* Phi;        // N x NX x nu : Phi_m = A^m B
+    // staged-kernel layout (capi.hip::stage_layout); staged == 0 -> dense kernel only
+    int32_t staged;           // layout present (nu == 2, compiled N, rows fit)
+    int32_t srs;              // row slots per lane
+    const double* s_coef;     // srs*64 x NX   row coefficients per (slot, lane)
+    const double* s_w0;       // srs*64
+    const double* s_E;        // srs*64 x NX
+    const int32_t* s_valid;   // srs*64
+    const double* phi_ac;     // (N+1) x 8: zero block, then Phi_m as [a][c]
+    const double* phi_ca;     // (N+1) x 8: zero block, then Phi_m as [c][a]
+    const double* s_mats;     // Q 16, P 16 (symmetrised), A 16, B 8, R 4
+    // opposite-row pairs (an equality written as two rows, e.g. the goal-box fallback
+    // terminal set, mpc.py:107-117); nullptr when the problem has none
+    const int32_t* partner;   // p: packed index of the opposite row or -1 (dense kernel)
+    const int32_t* s_partner; // srs*64: slot index of the opposite row or -1 (staged kernel)
 };
 
 struct Settings {
     double tol, tol_mu;
     int32_t max_iter;
-    int32_t kernel;
+    int32_t kernel;   // CARMPC_KERNEL_*: 0 auto (staged when available), 1 dense, 2 staged, 3 dense 4-wave
 };
 
 
@@ -91,5 +105,12 @@ hipError_t launch_dense(const DevProblem& P, int64_t batch, const double* x0, co
                         const Settings& s, hipStream_t stream, int* unsupported);
 bool dense_supported(int nv, int p, size_t* lds_bytes);
 int dense_pick_nv(int n);
+
+// Stage-structured kernel (ipm_staged.hip).
+constexpr int kStagedMaxRS = 4;
+bool staged_supported_N(int N);
+hipError_t launch_staged(const DevProblem& P, int64_t batch, const double* x0, const double* xref,
+                         double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
+                         const Settings& s, hipStream_t stream, int* unsupported);
 
 }  // namespace carmpc

@@ -454,13 +454,29 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
                 W.gmul(act ? v0 : 0.0, gx);
                 double viol = boxact ? fmax(v0 - ub, lb - v0) : -INFINITY;
                 double wsc = boxact ? bndabs : 0.0, ysc = fmax(fabs(v1), fabs(v2)), ymin = fmin(v1, v2);
+                // rows whose opposite partner is also active form an equality: their
+                // multipliers may be re-split, so they skip the sign test (oracle/qp.py)
+                bool paired[RS];
+#pragma unroll
+                for (int s = 0; s < RS; ++s) paired[s] = false;
+                if (P.partner) {
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int s = 0; s < RS; ++s) W.rvec[s * 64 + lane] = (W.rv[s] && dg[s] != 0.0) ? ra[s] : NAN;
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int s = 0; s < RS; ++s) {
+                        const int pr = W.rv[s] ? P.partner[s * 64 + lane] : -1;
+                        paired[s] = pr >= 0 && dg[s] != 0.0 && !isnan(W.rvec[pr]);
+                    }
+                }
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
                     if (W.rv[s]) {
                         viol = fmax(viol, gx[s] - w[s]);
                         wsc = fmax(wsc, fabs(w[s]));
                         ysc = fmax(ysc, fabs(ra[s]));
-                        ymin = fmin(ymin, ra[s]);
+                        ymin = paired[s] ? ymin : fmin(ymin, ra[s]);
                     }
                 }
                 const bool fin = !act || isfinite(v0);

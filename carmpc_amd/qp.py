@@ -55,6 +55,7 @@ class SolverSettings:
     tol: float = 1e-10
     tol_mu: float = 1e-12
     max_iter: int = 60
+    #: 0 auto (staged when the problem has a stage layout), 1 dense, 2 staged, 3 dense 4-wave
     kernel: int = 0
 
     def c(self) -> Settings:
@@ -118,6 +119,8 @@ class QPProblem:
         vals = [ctypes.c_int32() for _ in range(5)]
         check(_native.load().carmpc_problem_info(self._h, *[ctypes.byref(v) for v in vals]), "carmpc_problem_info")
         self.n, self.p, self.npre, self.nx, _ = (v.value for v in vals)
+        #: solve kernel chosen by ``kernel=0`` (auto): 1 dense, 2 staged
+        self.kernel = int(_native.load().carmpc_problem_kernel(self._h))
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -148,6 +151,10 @@ class QPProblem:
     def canonical_flops_per_iter(self) -> float:
         """p n^2 + n^3/3 + 6 n^2 + 12 p n with p = general (QP) rows."""
         return float(_native.load().carmpc_canonical_flops_per_iter(self.n, self.p))
+
+    def executed_flops_per_iter(self, kernel: int = 0) -> float:
+        """Flops per IPM iteration the chosen kernel actually executes."""
+        return float(_native.load().carmpc_executed_flops_per_iter(self._h, kernel))
 
     # ----------------------------------------------------------------- solve
     def solve(self, x0: torch.Tensor, xref: torch.Tensor | None = None, settings: SolverSettings | None = None,

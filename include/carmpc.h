@@ -84,8 +84,17 @@ typedef struct {
     double tol;        /* primal/dual residual tolerance, relative to 1+||.||_inf */
     double tol_mu;     /* complementarity tolerance (absolute)                     */
     int32_t max_iter;
-    int32_t kernel;    /* 0 = auto, 1 = dense (G,H in LDS), 2 = staged (structure) */
+    int32_t kernel;    /* 0 = auto (staged when the problem has one), 1 = dense (G,H in
+                          LDS), 2 = staged (stage structure, assembled problems with nu=2
+                          and a compiled N), 3 = dense with 4 waves per workgroup */
 } carmpc_settings;
+
+/* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged. */
+int carmpc_problem_kernel(const carmpc_problem* prob);
+
+/* Flops per IPM iteration the given kernel (0 auto, 1 dense, 2 staged) executes; the
+ * canonical dense count of SURVEY §8d is carmpc_canonical_flops_per_iter. */
+double carmpc_executed_flops_per_iter(const carmpc_problem* prob, int32_t kernel);
 
 /* Build one problem on the current device (assembly kernel + row normalisation). */
 int carmpc_problem_create(const carmpc_model_desc* desc, carmpc_problem** out);

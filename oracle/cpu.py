@@ -27,7 +27,7 @@ def load():
         dp = ctypes.POINTER(ctypes.c_double)
         ip = ctypes.POINTER(ctypes.c_int32)
         lib.oracle_solve_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp, dp, dp, dp,
-                                           dp, dp, dp, ctypes.c_int64, dp, dp, dp, ip, ip,
+                                           dp, dp, ip, dp, ctypes.c_int64, dp, dp, dp, ip, ip,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         lib.oracle_solve_batch.restype = ctypes.c_int
         _lib = lib
@@ -53,6 +53,7 @@ class CpuProblem:
         self.lb = None if asm.lb is None else np.ascontiguousarray(asm.lb)
         self.ub = None if asm.ub is None else np.ascontiguousarray(asm.ub)
         self.goal = np.ascontiguousarray(asm.goal, dtype=np.float64)
+        self.partner = np.ascontiguousarray(oq.opposite_pairs(Gn, w0n, En), dtype=np.int32)
 
     def solve(self, x0, xref=None, tol=oq.TOL_RES, tol_mu=oq.TOL_MU, max_iter=oq.MAX_ITER, threads=0):
         lib = load()
@@ -62,7 +63,8 @@ class CpuProblem:
         u = np.zeros((B, self.n)); st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
         rc = lib.oracle_solve_batch(self.n, self.G.shape[0], self.pre_w0.shape[0], _p(self.H), _p(self.G),
                                     _p(self.w0), _p(self.E), _p(self.pre_w0), _p(self.pre_E), _p(self.hq),
-                                    _p(self.lb), _p(self.ub), _p(self.goal), B, _p(x0), _p(xr), _p(u),
+                                    _p(self.lb), _p(self.ub), _p(self.partner, ctypes.c_int32), _p(self.goal), B,
+                                    _p(x0), _p(xr), _p(u),
                                     _p(st, ctypes.c_int32), _p(it, ctypes.c_int32), tol, tol_mu, max_iter, threads)
         assert rc == 0
         return u, st, it

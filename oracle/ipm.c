@@ -36,6 +36,7 @@
 typedef struct {
     int n, p, boxed;
     const double *H, *G, *lb, *ub;
+    const int32_t* partner;   /* opposite row (equality pair) or -1; NULL = none (qp.py::opposite_pairs) */
 } qp_t;
 
 static double maxstep(const double* v, const double* dv, int k, double cur) {
@@ -198,7 +199,10 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
         if (fabs(w[r]) > wsc) wsc = fabs(w[r]);
         if (gx[r] - w[r] > viol) viol = gx[r] - w[r];
         if (fabs(yg[r]) > ysc) ysc = fabs(yg[r]);
-        if (yg[r] < ymin) ymin = yg[r];
+        /* both rows of an opposite pair active = an equality: multipliers re-splittable */
+        const int pr = P->partner ? P->partner[r] : -1;
+        const int paired = pr >= 0 && dg[r] != 0.0 && dg[pr] != 0.0;
+        if (!paired && yg[r] < ymin) ymin = yg[r];
     }
     for (int i = 0; i < n; ++i) {
         if (!isfinite(x[i])) return 0;
@@ -410,14 +414,15 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
 }
 
 /* Batched entry point.  Arrays are row-major fp64.  lb/ub NULL => no input box.
+ * partner (p entries, -1 = none) or NULL: opposite-row pairs for the polish.
  * xref NULL => goal for every instance.  Returns 0, or -1 for n > 64. */
 int oracle_solve_batch(int n, int p, int npre, const double* H, const double* G, const double* w0,
                        const double* E, const double* pre_w0, const double* pre_E, const double* hq,
-                       const double* lb, const double* ub, const double* goal, int64_t B,
+                       const double* lb, const double* ub, const int32_t* partner, const double* goal, int64_t B,
                        const double* x0, const double* xref, double* u_out, int32_t* status,
                        int32_t* iters, double tol, double tol_mu, int max_iter, int nthreads) {
     if (n > 64) return -1;
-    qp_t P = {n, p, lb != NULL && ub != NULL, H, G, lb, ub};
+    qp_t P = {n, p, lb != NULL && ub != NULL, H, G, lb, ub, partner};
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else

@@ -52,11 +52,34 @@ def normalize_rows(G, w0, E):
             w0[~keep], E[~keep])
 
 
+def opposite_pairs(G, w0, E):
+    """partner[r] = r' if row r' is the exact negation of row r (G, w0 and E), else -1.
+
+    Such a pair writes an equality c'x = b as two inequalities -- the reference's
+    fallback terminal set x_N = goal (lib/mpc.py:107-117) does exactly that.  When both
+    rows are active the polish may re-split their multipliers."""
+    p = G.shape[0]
+    partner = np.full(p, -1, dtype=np.int32)
+    if p == 0:
+        return partner
+    rows = np.hstack([G, np.asarray(w0, float).reshape(-1, 1), E]) + 0.0   # + 0.0: -0.0 -> 0.0
+    neg = -rows + 0.0
+    key = {}
+    for r in range(p):
+        key.setdefault(rows[r].tobytes(), r)
+    for r in range(p):
+        r2 = key.get(neg[r].tobytes())
+        if r2 is not None and r2 != r:
+            partner[r] = r2
+    return partner
+
+
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
-        trace=None, refine=REFINE, polish=True, info=None):
+        trace=None, refine=REFINE, polish=True, info=None, partner=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
+    ``partner`` (``opposite_pairs``) marks rows that together form an equality.
     Returns (u, status, iterations, z_g)."""
     n = len(q)
     p = G.shape[0]
@@ -103,7 +126,8 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         if not np.isfinite(mu) or not np.isfinite(rdn):
             return u, STATUS_NUMERICAL, it, z
         if polish and rpn <= tol * pscale and rdn <= tol * dscale and mu <= POLISH_MU:
-            up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl)
+            up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
+                                 partner=partner)
             if info is not None:
                 info.setdefault("polish", []).append((it, ok))
             if ok:
@@ -163,17 +187,21 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         u = u + a * du; s = s + a * ds; z = z + a * dz
         su = su + a * dsu; zu = zu + a * dzu; sl = sl + a * dsl; zl = zl + a * dzl
     if polish:
-        up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl)
+        up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
+                             partner=partner)
         if ok:
             return up, STATUS_OPTIMAL, max_iter, z
     return u, STATUS_MAXITER, max_iter, z
 
 
-def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE):
+def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE,
+                partner=None):
     """Active-set polish.  Active set from the IPM iterate (s < z); solve the
     equality-constrained KKT [[H, A'], [A, 0]] [x; y] = [-q; b_act] by iterative refinement on
     the regularised factor  H + A'A/delta  (the IPM's M with d = 1/delta on active rows, 0 else);
-    accept only if x is primal feasible and the active multipliers are nonnegative."""
+    accept only if x is primal feasible and the active multipliers are nonnegative.  Rows whose
+    opposite partner is also active form an equality: their multipliers can be re-split as
+    (max(y-y',0), max(y'-y,0)) without changing A'y, so they are exempt from the sign test."""
     n = len(q)
     boxed = lb is not None
     dg = np.where(s < z, 1.0 / delta, 0.0)
@@ -209,7 +237,11 @@ def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, re
                        np.abs(lb).max() if boxed else 0.0)
     viol = max((G @ x - w).max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
                (lb - x).max() if boxed else -np.inf)
-    ymin = min(yg.min() if len(yg) else 0.0, yu.min() if boxed else 0.0, yl.min() if boxed else 0.0)
+    yg_sign = yg
+    if partner is not None and len(yg):
+        paired = ag & (partner >= 0) & ag[np.maximum(partner, 0)]
+        yg_sign = np.where(paired, 0.0, yg)
+    ymin = min(yg_sign.min() if len(yg) else 0.0, yu.min() if boxed else 0.0, yl.min() if boxed else 0.0)
     yscale = 1.0 + max(np.abs(yg).max() if len(yg) else 0.0, np.abs(yu).max() if boxed else 0.0,
                        np.abs(yl).max() if boxed else 0.0)
     ok = bool(viol <= POLISH_TOL * wscale and ymin >= -POLISH_TOL * yscale and np.all(np.isfinite(x)))
@@ -267,8 +299,13 @@ def certify(H, q, G, w, lb, ub, u_hint, act_tol=1e-7):
         sol = np.linalg.lstsq(KKT, np.hstack([-q, b[act]]), rcond=None)[0]
         ue, lam = sol[:n], sol[n:]
         viol = float(max((A @ ue - b).max(), 0.0)) if len(b) else 0.0
-        lmin = float(lam.min()) if k else 0.0
-        stn = float(np.abs(H @ ue + q + Aa.T @ lam).max())
+        # active opposite pairs (an equality written as two rows): re-split the multipliers
+        part = opposite_pairs(Aa, b[act], np.zeros((k, 0))) if k else np.zeros(0, np.int32)
+        lam_s = lam.copy()
+        for i in np.where(part >= 0)[0]:
+            lam_s[i] = max(lam[i] - lam[part[i]], 0.0)
+        lmin = float(lam_s.min()) if k else 0.0
+        stn = float(np.abs(H @ ue + q + Aa.T @ lam_s).max())
         ok = viol <= 1e-9 and lmin >= -1e-9 and stn <= 1e-9 * (1 + np.abs(q).max())
         if ok:
             return ue, True, (viol, lmin, stn)
@@ -305,6 +342,7 @@ def solve_instance(asm, x0, xref=None, info=None, **kw):
         out.update(status=STATUS_INFEASIBLE, iters=0, u=np.zeros(len(q)), u_exact=None,
                    certified=False, margin=float(pre.min()))
         return out
+    kw.setdefault("partner", opposite_pairs(Gn, w0n, En))
     u, st, it, _ = ipm(asm.H, q, Gn, wn, asm.lb, asm.ub, info=info, **kw)
     out.update(status=st, iters=it, u=u)
     if st == STATUS_OPTIMAL:

@@ -58,12 +58,28 @@ def test_assembly_kernel_matches_oracle(gpu_available, name, N):
     np.testing.assert_allclose(m["S"], golden["S"], rtol=0, atol=1e-13)
 
 
+KERNELS = [1, 2, 4]   # dense, staged (LDS Cholesky), staged (readlane Cholesky): carmpc_settings.kernel
+
+
+def _settings(kernel):
+    from carmpc_amd.qp import SolverSettings
+    return SolverSettings(kernel=kernel)
+
+
+def test_staged_layout_selected(gpu_available):
+    """Every reference configuration (N in {10, 20}, nu = 2) gets the staged kernel by default."""
+    for name, N in CONFIGS:
+        _, qp = _setup(name, N)
+        assert qp.kernel == 2, (name, N)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name,N", CONFIGS)
-def test_golden_vectors(gpu_available, name, N):
+def test_golden_vectors(gpu_available, name, N, kernel):
     import torch
     asm, qp = _setup(name, N)
     g = np.load(f"{GOLDEN}/qp_{name}_N{N}.npz")
-    u, st, it = qp.solve(torch.as_tensor(g["x0"]).cuda())
+    u, st, it = qp.solve(torch.as_tensor(g["x0"]).cuda(), settings=_settings(kernel))
     u, st, it = u.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
     np.testing.assert_array_equal(st, g["status"])
     ok = st == 0
@@ -84,15 +100,16 @@ def _random_x0(rng, goal_x, B):
                      rng.uniform(-np.pi / 8, np.pi / 8, B), rng.uniform(-1, 5, B)], axis=1)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name,N", CONFIGS)
-def test_random_batch_vs_c_oracle(gpu_available, name, N):
+def test_random_batch_vs_c_oracle(gpu_available, name, N, kernel):
     import torch
     from oracle.cpu import CpuProblem
     from oracle import qp as oq
     asm, qp = _setup(name, N)
     rng = np.random.default_rng(11 + N)
     X = _random_x0(rng, asm.goal[0], 2048)
-    u, st, it = qp.solve(torch.as_tensor(X).cuda())
+    u, st, it = qp.solve(torch.as_tensor(X).cuda(), settings=_settings(kernel))
     u, st = u.cpu().numpy(), st.cpu().numpy()
     uc, sc, ic = CpuProblem(asm).solve(X)
     agree = st == sc
@@ -159,13 +176,17 @@ def test_terminal_fallback_and_short_horizon(gpu_available, tmp_path):
         rng = np.random.default_rng(N)
         X = np.stack([rng.uniform(28, 30, 200), rng.uniform(1, 2, 200), rng.uniform(-0.05, 0.05, 200),
                       rng.uniform(-0.2, 0.2, 200)], axis=1)
-        u, st, _ = qp.solve(torch.as_tensor(X).cuda())
         uc, sc, _ = CpuProblem(asm).solve(X)
-        st = st.cpu().numpy()
-        assert (st == sc).mean() > 0.99
-        both = (st == 0) & (sc == 0)
-        if both.any():
-            assert np.abs(u.cpu().numpy()[both] - uc[both]).max() <= U_TOL
+        assert ((sc == 0) | (sc == 1)).all()   # equality pairs handled: no iteration-limit stops
+        if N == 10:
+            assert (sc == 0).all()
+        for kernel in [1] + ([2] if qp.kernel == 2 else []):
+            u, st, _ = qp.solve(torch.as_tensor(X).cuda(), settings=_settings(kernel))
+            st = st.cpu().numpy()
+            np.testing.assert_array_equal(st, sc, err_msg=f"N={N} kernel {kernel}")
+            ok = sc == 0
+            if ok.any():
+                assert np.abs(u.cpu().numpy()[ok] - uc[ok]).max() <= U_TOL
 
 
 def test_observer_and_plant_kernels(gpu_available):

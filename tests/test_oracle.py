@@ -143,3 +143,31 @@ def test_closed_loop_statefb_reproduces_golden_trace():
         assert r["status"] == 0
         u = r["u_exact"][:2] if r["certified"] else r["u"][:2]
     assert np.all(np.abs(state - asm.goal) <= 1e-1)
+
+
+def test_goal_box_fallback_equality_pairs(tmp_path):
+    """Without a terminal-set file the reference constrains x_N to the goal box written as
+    opposite row pairs (mpc.py:107-117): an equality with no strict interior.  The pairs are
+    detected and the polish re-splits their multipliers, so every instance is solved and
+    KKT-certified (before: iteration limit on ~1% of them)."""
+    from oracle.cpu import CpuProblem
+    asm = oa.build("RoadEnv", 10, terminal_set_dir=str(tmp_path))
+    Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
+    partner = oq.opposite_pairs(Gn, w0n, En)
+    paired = np.where(partner >= 0)[0]
+    assert len(paired) == 6 and np.array_equal(partner[partner[paired]], paired)
+    np.testing.assert_array_equal(Gn[paired], -Gn[partner[paired]])
+    rng = np.random.default_rng(10)
+    X = np.stack([rng.uniform(28, 30, 200), rng.uniform(1, 2, 200), rng.uniform(-0.05, 0.05, 200),
+                  rng.uniform(-0.2, 0.2, 200)], axis=1)
+    u, st, it = CpuProblem(asm).solve(X, threads=2)
+    assert (st == 0).all() and it.max() <= 20
+    for i in range(0, 200, 25):
+        r = oq.solve_instance(asm, X[i])
+        assert r["status"] == 0 and r["certified"] and r["iters"] == it[i]
+        assert np.abs(r["u_exact"] - u[i]).max() <= 1e-8
+    # the reference's own terminal sets have no such pairs
+    for name, N in CONFIGS:
+        a = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+        G2, w2, E2, *_ = oq.normalize_rows(a.G, a.w0, a.E)
+        assert (oq.opposite_pairs(G2, w2, E2) < 0).all()
