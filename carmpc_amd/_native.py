@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcarmpc.so")
+# CARMPC_LIB selects another in-tree build of the same ABI (e.g. the phase-timing
+# profiling build of tools/phase_timing.py); default: the production library.
+LIB_PATH = os.environ.get("CARMPC_LIB") or os.path.join(_HERE, "libcarmpc.so")
 
 # status codes (carmpc.h)
 OPTIMAL, PRIMAL_INFEASIBLE, MAX_ITER, NUMERICAL = 0, 1, 2, 3

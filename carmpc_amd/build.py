@@ -32,15 +32,20 @@ def _stale(obj, src):
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
-def build(verbose: bool = True, jobs: int = 4) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(verbose: bool = True, jobs: int = 4, variant: str = "") -> str:
+    """Compile csrc/*.hip for gfx950 and link the shared library.  variant="timing"
+    builds the phase-timing profiling library build/timing/libcarmpc.so instead."""
+    obj_dir = OBJ if not variant else os.path.join(REPO, "build", variant, "obj")
+    lib_path = LIB if not variant else os.path.join(REPO, "build", variant, "libcarmpc.so")
+    extra = {"": [], "timing": ["-DCARMPC_PHASE_TIMING"]}[variant]
+    os.makedirs(obj_dir, exist_ok=True)
     hipcc = _hipcc()
 
     def compile_one(src):
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJ, src.replace(".hip", ".o"))
+        o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         if _stale(o, s):
-            cmd = [hipcc, *FLAGS, "-c", s, "-o", o]
+            cmd = [hipcc, *FLAGS, *extra, "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
@@ -48,13 +53,13 @@ def build(verbose: bool = True, jobs: int = 4) -> str:
 
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB]
+    if not os.path.exists(lib_path) or any(os.path.getmtime(o) > os.path.getmtime(lib_path) for o in objs):
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", lib_path]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-    return LIB
+    return lib_path
 
 
 if __name__ == "__main__":
-    build(verbose="-q" not in sys.argv)
+    build(verbose="-q" not in sys.argv, variant="timing" if "--timing" in sys.argv else "")

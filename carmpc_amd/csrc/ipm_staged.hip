@@ -27,6 +27,32 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+// Optional per-phase cycle accounting (profiling build only: -DCARMPC_PHASE_TIMING,
+// tools/phase_timing.py).  Phases: 0 residuals, 1 Farkas/decisions, 2 M build,
+// 3 Cholesky, 4 right-hand sides, 5 triangular solves, 6 G dx + direction update,
+// 7 step / polish verification.
+#ifdef CARMPC_PHASE_TIMING
+__device__ unsigned long long carmpc_phase_cycles[8];
+#define PT_DECL                                   \
+    unsigned long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+    unsigned long long pt_t = clock64();
+#define PT_MARK(i)                                \
+    do {                                          \
+        const unsigned long long n_ = clock64();  \
+        pt_acc[i] += n_ - pt_t;                   \
+        pt_t = n_;                                \
+    } while (0)
+#define PT_FLUSH()                                                              \
+    do {                                                                        \
+        if (lane == 0)                                                          \
+            for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&carmpc_phase_cycles[i_], pt_acc[i_]); \
+    } while (0)
+#else
+#define PT_DECL
+#define PT_MARK(i) do {} while (0)
+#define PT_FLUSH() do {} while (0)
+#endif
+
 namespace carmpc {
 
 namespace {
@@ -42,21 +68,64 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// ---- cross-lane reductions without the LDS crossbar ---------------------------------
+// Butterfly pairings only (quad xor 1, quad xor 2, row half-mirror, row mirror, then the
+// gfx950 row-16 / half-32 swaps): both lanes of a pair combine the same two operands, so
+// every lane ends with a bitwise-identical result (the step length, mu and the Farkas
+// sums drive wave-uniform decisions).  ~3 VALU per step instead of a ds_bpermute round
+// trip per 32 bits.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+// the two operands of the row-16 pair (rows 0<->1, 2<->3) resp. the half-32 pair
+__device__ __forceinline__ void swap16_d(double v, double& a, double& b) {
+    const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(x >> 32), false, false);
+    a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+__device__ __forceinline__ void swap32_d(double v, double& a, double& b) {
+    const unsigned long long x = __builtin_bit_cast(unsigned long long, v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(x >> 32), false, false);
+    a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    b = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
 }
+constexpr int DPP_QXOR1 = 0xB1, DPP_QXOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+struct OpSum { __device__ static double f(double a, double b) { return a + b; } };
+struct OpMax { __device__ static double f(double a, double b) { return fmax(a, b); } };
+struct OpMin { __device__ static double f(double a, double b) { return fmin(a, b); } };
+// reduction over each 16-lane row
+template <class Op>
+__device__ __forceinline__ double row_reduce(double v) {
+    v = Op::f(v, dpp_d<DPP_QXOR1>(v));
+    v = Op::f(v, dpp_d<DPP_QXOR2>(v));
+    v = Op::f(v, dpp_d<DPP_HMIRROR>(v));
+    return Op::f(v, dpp_d<DPP_MIRROR>(v));
+}
+// reduction over each 32-lane half
+template <class Op>
+__device__ __forceinline__ double half_reduce(double v) {
+    v = row_reduce<Op>(v);
+    double a, b;
+    swap16_d(v, a, b);
+    return Op::f(a, b);
+}
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v) {
+    v = half_reduce<Op>(v);
+    double a, b;
+    swap32_d(v, a, b);
+    return Op::f(a, b);
+}
+__device__ __forceinline__ double wave_sum(double v) { return wave_reduce<OpSum>(v); }
+__device__ __forceinline__ double wave_max(double v) { return wave_reduce<OpMax>(v); }
+__device__ __forceinline__ double wave_min(double v) { return wave_reduce<OpMin>(v); }
 // Reciprocal / reciprocal square root: hardware approximation + two Newton steps
 // (to the last ulp or so; ~5 instructions instead of the ~10 of an IEEE divide).
 __device__ __forceinline__ double frcp(double b) {
@@ -80,8 +149,11 @@ __host__ __device__ constexpr int sym10(int a, int b) { return a * 4 - a * (a - 
 // Block-shared problem data (LDS).
 template <int N, int RS>
 struct StageShared {
-    double phi_ac[(N + 1) * 8];   // entry 0 = zeros; entry m+1 = Phi_m as [a][c]
-    double phi_ca[(N + 1) * 8];   // same as [c][a]
+    // Phi_m = A^m B tables indexed by a shifted q in [0, 2N-2] so that every gather in a
+    // loop over stages is lane_base + (compile-time offset): no per-step index math.
+    double fa[(2 * N - 1) * 8];   // [c][a]: Phi_{q-(N-1)} for q >= N-1, else 0
+    double fb[(2 * N - 1) * 8];   // [c][a]: Phi_{(N-1)-q} for q <  N-1, else 0
+    double fs[(2 * N - 1) * 8];   // [a][c]: Phi_{(N-1)-q} for q <= N-1, else 0
     double2 cf01[RS * 64];        // row coefficients (c0, c1) of slot (s, lane)
     double2 cf23[RS * 64];        // (c2, c3)
     double qp[2][16];             // Q (stages < N), P (stage N)
@@ -96,7 +168,7 @@ struct StageWave {
     double Y[(N + 1) * 4];        // predicted states Y_k (k = 1..N)
     double lam[(N + 1) * 4];      // adjoint input lam_k
     double lamH[(N + 1) * 4];     // second adjoint input (residual: H part)
-    double Wf[(N + 1) * 10];      // W_k packed symmetric
+    double Wf[(N + 1) * 10 >= 64 ? (N + 1) * 10 : 64];   // W_k packed symmetric; 2nd Cholesky buffer
     double Z[N * 16];             // Z_t (t = 0..N-1)
     double Gam[N * 8];            // Gam_t[c][a] = (B' Z_t)[c][a]
     double w[RS * 64];            // w = w0 - E x0 per row slot
@@ -132,20 +204,19 @@ struct StageCtx {
         const int ap = L & 1;
         const int yk = L < 2 * N ? (L >> 1) + 1 : 1;
         const double2* v2 = reinterpret_cast<const double2*>(wv->bvec);
-        double y0 = 0.0, y1 = 0.0;
+        double y0 = 0.0, y1 = 0.0, z0 = 0.0, z1 = 0.0;   // split chains
+        const double* fbase = sh->fs + (N - yk) * 8 + ap * 4;   // q = t + N - yk: Phi_{yk-1-t}
 #pragma unroll 4
         for (int t = 0; t < N; ++t) {
-            int m = yk - 1 - t;
-            m = m < -1 ? -1 : m;
-            const double2* ph = reinterpret_cast<const double2*>(sh->phi_ac + (m + 1) * 8 + ap * 4);
+            const double2* ph = reinterpret_cast<const double2*>(fbase + t * 8);
             const double2 a = ph[0], b = ph[1];
             const double2 vv = v2[t];
             y0 = fma(a.x, vv.x, y0);
-            y0 = fma(a.y, vv.y, y0);
+            z0 = fma(a.y, vv.y, z0);
             y1 = fma(b.x, vv.x, y1);
-            y1 = fma(b.y, vv.y, y1);
+            z1 = fma(b.y, vv.y, z1);
         }
-        if (L < 2 * N) reinterpret_cast<double2*>(wv->Y)[yk * 2 + ap] = make_double2(y0, y1);
+        if (L < 2 * N) reinterpret_cast<double2*>(wv->Y)[yk * 2 + ap] = make_double2(y0 + z0, y1 + z1);
         __builtin_amdgcn_wave_barrier();
     }
     __device__ __forceinline__ void rows_from_Y(double (&out)[RS]) const {
@@ -182,13 +253,15 @@ struct StageCtx {
     template <int K>
     __device__ __forceinline__ void stage_reduce(double (&v)[K]) const {
 #pragma unroll
-        for (int e = 0; e < K; ++e) v[e] += __shfl_xor(v[e], 32, 64);
+        for (int e = 0; e < K; ++e) {
+            double a, b;
+            swap32_d(v[e], a, b);   // lanes L and L^32 hold rows of the same stage
+            v[e] = a + b;
+        }
         if (N < 32) {
 #pragma unroll
             for (int e = 0; e < K; ++e) {
-                double t = tail ? v[e] : 0.0;
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+                const double t = half_reduce<OpSum>(tail ? v[e] : 0.0);
                 v[e] += (lane == N - 1) ? t : 0.0;
             }
         }
@@ -247,47 +320,45 @@ struct StageCtx {
     __device__ __forceinline__ double adjoint(const double* lp) const {
         const int L = olane();
         const int vt = var_t(L), vc = L & 1;
-        double g = 0.0;
+        double g = 0.0, h = 0.0;   // two chains: shorter FMA dependency
+        const double* fbase = sh->fa + (N - 1 - vt) * 8 + vc * 4;   // q = k-1 + N-1-vt: Phi_{k-1-vt}
 #pragma unroll 4
         for (int k = 1; k <= N; ++k) {
-            int m = k - 1 - vt;
-            m = m < -1 ? -1 : m;
-            const double2* ph = reinterpret_cast<const double2*>(sh->phi_ca + (m + 1) * 8 + vc * 4);
+            const double2* ph = reinterpret_cast<const double2*>(fbase + (k - 1) * 8);
             const double2 p0 = ph[0], p1 = ph[1];
             const double2* l2 = reinterpret_cast<const double2*>(lp + k * 4);
             const double2 l0 = l2[0], l1 = l2[1];
             g = fma(p0.x, l0.x, g);
-            g = fma(p0.y, l0.y, g);
+            h = fma(p0.y, l0.y, h);
             g = fma(p1.x, l1.x, g);
-            g = fma(p1.y, l1.y, g);
+            h = fma(p1.y, l1.y, h);
         }
-        return act ? g : 0.0;
+        return act ? g + h : 0.0;
     }
     // two adjoints sharing the Phi gathers
     __device__ __forceinline__ void adjoint2(const double* lp, const double* lq, double& g1, double& g2) const {
         const int L = olane();
         const int vt = var_t(L), vc = L & 1;
-        double a1 = 0.0, a2 = 0.0;
+        double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+        const double* fbase = sh->fa + (N - 1 - vt) * 8 + vc * 4;
 #pragma unroll 4
         for (int k = 1; k <= N; ++k) {
-            int m = k - 1 - vt;
-            m = m < -1 ? -1 : m;
-            const double2* ph = reinterpret_cast<const double2*>(sh->phi_ca + (m + 1) * 8 + vc * 4);
+            const double2* ph = reinterpret_cast<const double2*>(fbase + (k - 1) * 8);
             const double2 p0 = ph[0], p1 = ph[1];
             const double2* l2 = reinterpret_cast<const double2*>(lp + k * 4);
             const double2* q2 = reinterpret_cast<const double2*>(lq + k * 4);
             const double2 l0 = l2[0], l1 = l2[1], q0 = q2[0], q1 = q2[1];
             a1 = fma(p0.x, l0.x, a1);
-            a1 = fma(p0.y, l0.y, a1);
+            b1 = fma(p0.y, l0.y, b1);
             a1 = fma(p1.x, l1.x, a1);
-            a1 = fma(p1.y, l1.y, a1);
+            b1 = fma(p1.y, l1.y, b1);
             a2 = fma(p0.x, q0.x, a2);
-            a2 = fma(p0.y, q0.y, a2);
+            b2 = fma(p0.y, q0.y, b2);
             a2 = fma(p1.x, q1.x, a2);
-            a2 = fma(p1.y, q1.y, a2);
+            b2 = fma(p1.y, q1.y, b2);
         }
-        g1 = act ? a1 : 0.0;
-        g2 = act ? a2 : 0.0;
+        g1 = act ? a1 + b1 : 0.0;
+        g2 = act ? a2 + b2 : 0.0;
     }
 
     // ---- normal matrix -----------------------------------------------------------------
@@ -367,14 +438,14 @@ struct StageCtx {
         const double2 g01 = gs2[0], g23 = gs2[1];
         const double rr0 = vc ? sh->R[1] : sh->R[0];   // R[0][c]
         const double rr1 = vc ? sh->R[3] : sh->R[2];   // R[1][c]
+        const double* abase = sh->fa + (N - 1 - vt) * 8 + vc * 4;   // q = t + N-1-vt
+        const double* bbase = sh->fb + (N - 1 - vt) * 8;
 #pragma unroll
         for (int t = 0; t < N; ++t) {
             const int d = t - vt;
-            const int iA = (d >= 0 ? d : -1) + 1;
-            const int iB = (d < 0 ? -d : -1) + 1;
-            const double2* pa2 = reinterpret_cast<const double2*>(sh->phi_ca + iA * 8 + vc * 4);
+            const double2* pa2 = reinterpret_cast<const double2*>(abase + t * 8);   // Phi_d (d >= 0)
             const double2 fa0 = pa2[0], fa1 = pa2[1];
-            const double2* pb2 = reinterpret_cast<const double2*>(sh->phi_ca + iB * 8);
+            const double2* pb2 = reinterpret_cast<const double2*>(bbase + t * 8);   // Phi_{-d} (d < 0)
             const double2 fb00 = pb2[0], fb01 = pb2[1], fb10 = pb2[2], fb11 = pb2[3];
             const double2* gt2 = reinterpret_cast<const double2*>(wv->Gam + t * 8);
             const double2 G00 = gt2[0], G01 = gt2[1], G10 = gt2[2], G11 = gt2[3];
@@ -424,7 +495,7 @@ __device__ __forceinline__ double cholesky_lds(double (&M)[NV], int lane, double
 #pragma unroll
             for (int j = k + 1; j < NV; ++j) M[j] = fma(-col[j], l, M[j]);
         }
-        M[k] = (lane == k) ? lkk : (below ? l : M[k]);
+        M[k] = (lane == k) ? lkk : (below ? l * inv : M[k]);   // row part: L~ = L / l_kk
         inv_ii = (lane == k) ? inv : inv_ii;
     }
     __builtin_amdgcn_wave_barrier();
@@ -447,31 +518,33 @@ __device__ __forceinline__ double cholesky(double (&M)[NV], int lane) {
         const double lt = l * inv;
 #pragma unroll
         for (int j = k + 1; j < NV; ++j) M[j] = fma(-readlane_d(M[j], k), lt, M[j]);
-        M[k] = (lane == k) ? lkk : (below ? l : M[k]);
+        M[k] = (lane == k) ? lkk : (below ? lt : M[k]);   // row part: L~ = L / l_kk
         inv_ii = (lane == k) ? inv : inv_ii;
     }
     return inv_ii;
 }
 
+// Solve M x = b with M = L~ D^2 L~' (L~ unit lower, D = diag(l_kk)) in the slot layout:
+// lane i's slot j < i holds L~[i][j], slot j > i holds l_ii L[j][i] = l_ii^2 L~[j][i], and
+// inv2 = 1 / l_ii^2.  b per lane, lanes >= NV pass 0.
 template <int NV>
-__device__ __forceinline__ double chol_solve(const double (&M)[NV], double inv_ii, double b, int lane) {
+__device__ __forceinline__ double chol_solve(const double (&M)[NV], double inv2, double b, int lane) {
     asm volatile("" : "+v"(lane));
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        const double yk = readlane_d(b * inv_ii, k);
+    for (int k = 0; k < NV; ++k) {   // forward, unit diagonal: w = L~^{-1} b
+        const double yk = readlane_d(b, k);
         const double upd = fma(M[k], -yk, b);
         b = (lane > k) ? upd : b;
-        b = (lane == k) ? yk : b;
     }
-    double acc = 0.0;
+    const double v = b * inv2;       // D^{-2} w
+    double acc = 0.0;                // sum_{j>i} slot_j x_j
 #pragma unroll
-    for (int k = NV - 1; k >= 0; --k) {
-        const double xk = readlane_d((b - inv_ii * acc) * inv_ii, k);
+    for (int k = NV - 1; k >= 0; --k) {   // backward: x_k = v_k - inv2_k acc_k
+        const double xk = readlane_d(fma(-inv2, acc, v), k);
         const double upd = fma(M[k], xk, acc);
-        b = (lane == k) ? xk : b;
         acc = (lane < k) ? upd : acc;
     }
-    return lane < NV ? b : 0.0;
+    return lane < NV ? fma(-inv2, acc, v) : 0.0;
 }
 
 }  // namespace
@@ -487,9 +560,12 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
     __shared__ __attribute__((aligned(16))) StageWave<N, RS> wscr[kWPB];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < (N + 1) * 8; i += blockDim.x) {
-        sh.phi_ac[i] = P.phi_ac[i];
-        sh.phi_ca[i] = P.phi_ca[i];
+    for (int i = threadIdx.x; i < (2 * N - 1) * 8; i += blockDim.x) {
+        const int q = i >> 3, e = i & 7;
+        const int mf = q - (N - 1), mr = (N - 1) - q;   // P.phi_*: entry m+1 = Phi_m
+        sh.fa[i] = mf >= 0 ? P.phi_ca[(mf + 1) * 8 + e] : 0.0;
+        sh.fb[i] = mr > 0 ? P.phi_ca[(mr + 1) * 8 + e] : 0.0;
+        sh.fs[i] = mr >= 0 ? P.phi_ac[(mr + 1) * 8 + e] : 0.0;
     }
     for (int i = threadIdx.x; i < RS * 64; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.s_coef[i * 4 + 0], P.s_coef[i * 4 + 1]);
@@ -584,6 +660,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
         int it = 0;
         bool polish_failed = false;
         double M[NV];
+        PT_DECL
         for (;;) {
             double rp[RS];
             double gtz, rd, rpu, rpl, mu;
@@ -619,6 +696,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                 if (!isfinite(mu) || !isfinite(rdn_w)) { status = CARMPC_NUMERICAL; break; }
                 res_ok = rpn_w <= S.tol * pscale && rdn_w <= S.tol * dscale;
             }
+            PT_MARK(0);
             const bool last = it >= S.max_iter;
             const bool polish = !polish_failed && ((res_ok && mu <= POLISH_MU) || last);
             if (!polish) {
@@ -645,8 +723,12 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
             for (int s = 0; s < RS; ++s)
                 wv.dg[s * 64 + lane] = !W.rv[s] ? 0.0 : (polish ? (s_[s] < z_[s] ? id : 0.0) : z_[s] * frcp(s_[s]));
             __builtin_amdgcn_wave_barrier();
+            PT_MARK(1);
             W.build_M(M, polish ? dbu + dbl : (boxact ? zu * frcp(su) + zl * frcp(sl) : 0.0));
+            PT_MARK(2);
             const double inv_ii = kLdsChol ? cholesky_lds<NV>(M, lane, wv.bvec) : cholesky<NV>(M, lane);
+            const double inv2 = inv_ii * inv_ii;
+            PT_MARK(3);
             // row temporaries: ra = dS | y_g ; rb = dZ | ry_g ; (LDS) pa = dS_aff dZ_aff
             double ra[RS], rb[RS];
 #pragma unroll
@@ -692,7 +774,9 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                     const double hg = W.adjoint(wv.lam);
                     rhs = act ? -(hg + rdu + rd + (boxact ? v3 - v4 : 0.0)) : 0.0;
                 }
-                const double sol = chol_solve<NV>(M, inv_ii, rhs, lane);
+                PT_MARK(4);
+                const double sol = chol_solve<NV>(M, inv2, rhs, lane);
+                PT_MARK(5);
                 double gs[RS];
                 W.gmul(sol, gs);
                 if (polish) {
@@ -745,6 +829,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                     }
                 }
             }
+            PT_MARK(6);
             if (polish) {
                 double gx[RS];
                 W.gmul(act ? v0 : 0.0, gx);
@@ -796,7 +881,10 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
             su += a * v1; zu += a * v3; sl += a * v2; zl += a * v4;
             polish_failed = false;
             ++it;
+            PT_MARK(7);
         }
+        PT_MARK(7);
+        PT_FLUSH();
         if (lane < P.n) u_out[inst * ld_u + lane] = u;
         if (lane == 0) {
             status_out[inst] = status;
@@ -881,3 +969,16 @@ hipError_t launch_staged(const DevProblem& P, int64_t batch, const double* x0, c
 }
 
 }  // namespace carmpc
+
+#ifdef CARMPC_PHASE_TIMING
+// Profiling build only: read (and optionally reset) the per-phase cycle counters.
+extern "C" int carmpc_debug_phase_cycles(unsigned long long* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(carmpc_phase_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(carmpc_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
