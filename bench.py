@@ -172,11 +172,13 @@ def main():
     value = total / wall_max
     status_split = {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
                                                                       "numerical"))}
-    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 4: "ipm_staged_readlane"}
+    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 4: "ipm_staged_readlane", 5: "ipm_staged_4wave", 6: "ipm_staged_ldl"}
     kdesc = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
              2: "ipm_staged (wavefront per QP, stage-structured G/H products and Riccati-style M build)",
              3: "ipm_dense, 4 waves per workgroup",
-             4: "ipm_staged with the readlane-broadcast Cholesky (A/B variant)"}
+             4: "ipm_staged with the readlane-broadcast Cholesky (A/B variant)",
+             5: "ipm_staged, 4 waves per workgroup (512 registers per wave)",
+             6: "ipm_staged with the square-root-free LDL' (A/B variant)"}
     used = sorted(set(kernels))
     out = {
         "metric": "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X",

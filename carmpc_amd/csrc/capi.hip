@@ -244,7 +244,7 @@ int stage_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vecto
 hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, const double* xref, double* u_out,
                         int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
-    const bool staged = s.kernel == 2 || s.kernel == 4 || (s.kernel == 0 && D.staged);
+    const bool staged = (s.kernel >= 4 && s.kernel <= 6) || s.kernel == 2 || (s.kernel == 0 && D.staged);
     if (staged) return launch_staged(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     return launch_dense(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
 }
@@ -265,7 +265,7 @@ int carmpc_problem_kernel(const carmpc_problem* P) {
 double carmpc_executed_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
     if (!P) return 0.0;
     const double n = P->dev.n, p = P->dev.p, N = P->dev.N;
-    const bool staged = kernel == 2 || kernel == 4 || (kernel == 0 && P->dev.staged);
+    const bool staged = (kernel >= 4 && kernel <= 6) || kernel == 2 || (kernel == 0 && P->dev.staged);
     const double chol = n * n * n / 3.0, trisolve = 2.0 * n * n;
     if (!staged) {
         const double gv = 2.0 * p * n, hv = 2.0 * n * n;

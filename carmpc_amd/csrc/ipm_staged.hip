@@ -116,12 +116,19 @@ __device__ __forceinline__ double half_reduce(double v) {
     swap16_d(v, a, b);
     return Op::f(a, b);
 }
+// the result is identical in all lanes: hand it to the compiler as a scalar (SGPR pair)
+__device__ __forceinline__ double uniform_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 template <class Op>
 __device__ __forceinline__ double wave_reduce(double v) {
     v = half_reduce<Op>(v);
     double a, b;
     swap32_d(v, a, b);
-    return Op::f(a, b);
+    return uniform_d(Op::f(a, b));
 }
 __device__ __forceinline__ double wave_sum(double v) { return wave_reduce<OpSum>(v); }
 __device__ __forceinline__ double wave_max(double v) { return wave_reduce<OpMax>(v); }
@@ -160,6 +167,7 @@ struct StageShared {
     double A[16];
     double B[8];                  // [a][c]
     double R[4];
+    double lb[64], ub[64];        // input box per variable (+-UNBOXED_BOUND when unboxed)
 };
 // Per-wave scratch (LDS).
 template <int N, int RS>
@@ -173,6 +181,7 @@ struct StageWave {
     double Gam[N * 8];            // Gam_t[c][a] = (B' Z_t)[c][a]
     double w[RS * 64];            // w = w0 - E x0 per row slot
     double pa[RS * 64];           // predictor products dS_aff dZ_aff
+    double rp[RS * 64];           // primal residual G u + s - w of the current iterate
     double dg[RS * 64];           // row weights of the current factorization
 };
 
@@ -436,8 +445,9 @@ struct StageCtx {
         const int vt = var_t(L), vc = L & 1;
         const double2* gs2 = reinterpret_cast<const double2*>(wv->Gam + vt * 8 + vc * 4);
         const double2 g01 = gs2[0], g23 = gs2[1];
-        const double rr0 = vc ? sh->R[1] : sh->R[0];   // R[0][c]
-        const double rr1 = vc ? sh->R[3] : sh->R[2];   // R[1][c]
+        // diagonal 2x2 block: R[c'][c] plus the box barrier on the diagonal entry c' == c
+        const double rr0 = (vc ? sh->R[1] : sh->R[0]) + (vc ? 0.0 : dbox);   // R[0][c]
+        const double rr1 = (vc ? sh->R[3] : sh->R[2]) + (vc ? dbox : 0.0);   // R[1][c]
         const double* abase = sh->fa + (N - 1 - vt) * 8 + vc * 4;   // q = t + N-1-vt
         const double* bbase = sh->fb + (N - 1 - vt) * 8;
 #pragma unroll
@@ -468,16 +478,45 @@ struct StageCtx {
             M[2 * t] = m0 + (d == 0 ? rr0 : 0.0);
             M[2 * t + 1] = m1 + (d == 0 ? rr1 : 0.0);
         }
-#pragma unroll
-        for (int j = 0; j < NV; ++j) M[j] += (j == L) ? dbox : 0.0;
     }
 };
 
-// Guarded right-looking Cholesky in the slot layout, column k broadcast through LDS:
-// every lane writes L[lane][k] once, then reads L[j][k] (j > k) with b128 broadcasts.
-// The LDS pipe carries the broadcast instead of 2(NV-k) v_readlane + hazard nops.
+// Guarded square-root-free LDL' in the slot layout (M = L~ D L~', D = diag(d_k)), the
+// UNSCALED column k broadcast through LDS: every lane publishes c_i = M_i[k] once, then
+// reads c_j (j > k) with b128 broadcasts; lane i updates with t_i = c_i / d_k.  One
+// reciprocal per step and no diagonal store (the solves use 1/d_i).  Result layout:
+// lane i's slot j < i = L~[i][j]; slot j > i = d_i L~[j][i]; returns 1/d_lane.
 template <int NV>
 __device__ __forceinline__ double cholesky_lds(double (&M)[NV], int lane, double* col) {
+    asm volatile("" : "+v"(lane));
+    double invd = 1.0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double piv = readlane_d(M[k], k);
+        if (!(piv > 0.0)) piv = 1e128;
+        const double rp = frcp(piv);
+        const bool below = lane > k && lane < NV;
+        const double t = below ? M[k] * rp : 0.0;      // L~[lane][k]
+        if (k + 1 < NV) {
+            __builtin_amdgcn_wave_barrier();
+            // lanes <= k write t (never read): the store, and with it the broadcast reads,
+            // wait for the reciprocal, so the column is not held in registers meanwhile
+            col[lane] = below ? M[k] : t;
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = k + 1; j < NV; ++j) M[j] = fma(-col[j], t, M[j]);
+        }
+        M[k] = below ? t : M[k];
+        invd = (lane == k) ? rp : invd;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return invd;
+}
+
+// Cholesky with square roots, scaled column L[.][k] broadcast through LDS (same result
+// layout as cholesky_lds: row part L~, column part d_i L~; returns 1/d_lane).
+template <int NV>
+__device__ __forceinline__ double cholesky_lds_sqrt(double (&M)[NV], int lane, double* col) {
     asm volatile("" : "+v"(lane));
     double inv_ii = 1.0;
 #pragma unroll
@@ -495,11 +534,11 @@ __device__ __forceinline__ double cholesky_lds(double (&M)[NV], int lane, double
 #pragma unroll
             for (int j = k + 1; j < NV; ++j) M[j] = fma(-col[j], l, M[j]);
         }
-        M[k] = (lane == k) ? lkk : (below ? l * inv : M[k]);   // row part: L~ = L / l_kk
+        M[k] = (lane == k) ? lkk : (below ? l * inv : M[k]);
         inv_ii = (lane == k) ? inv : inv_ii;
     }
     __builtin_amdgcn_wave_barrier();
-    return inv_ii;
+    return inv_ii * inv_ii;
 }
 
 // Same factorization with the column broadcast by v_readlane (kernel id 4, for A/B).
@@ -521,7 +560,7 @@ __device__ __forceinline__ double cholesky(double (&M)[NV], int lane) {
         M[k] = (lane == k) ? lkk : (below ? lt : M[k]);   // row part: L~ = L / l_kk
         inv_ii = (lane == k) ? inv : inv_ii;
     }
-    return inv_ii;
+    return inv_ii * inv_ii;   // 1/d_lane, d = l^2
 }
 
 // Solve M x = b with M = L~ D^2 L~' (L~ unit lower, D = diag(l_kk)) in the slot layout:
@@ -549,13 +588,13 @@ __device__ __forceinline__ double chol_solve(const double (&M)[NV], double inv2,
 
 }  // namespace
 
-template <int N, int RS, bool kLdsChol>
-__global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t batch, const double* __restrict__ x0,
+// kChol: 0 readlane broadcast, 1 LDS broadcast with square roots, 2 LDS square-root-free LDL'
+template <int N, int RS, int kChol, int kWPB>
+__global__ void __launch_bounds__(kWPB * 64) ipm_staged_kernel(DevProblem P, int64_t batch, const double* __restrict__ x0,
                                                          const double* __restrict__ xref, double* __restrict__ u_out,
                                                          int64_t ld_u, int32_t* __restrict__ status_out,
                                                          int32_t* __restrict__ iters_out, Settings S) {
     constexpr int NV = 2 * N;
-    constexpr int kWPB = 8;
     __shared__ __attribute__((aligned(16))) StageShared<N, RS> sh;
     __shared__ __attribute__((aligned(16))) StageWave<N, RS> wscr[kWPB];
     const int lane = threadIdx.x & 63;
@@ -570,6 +609,11 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
     for (int i = threadIdx.x; i < RS * 64; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.s_coef[i * 4 + 0], P.s_coef[i * 4 + 1]);
         sh.cf23[i] = make_double2(P.s_coef[i * 4 + 2], P.s_coef[i * 4 + 3]);
+    }
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) {
+        const bool bx = i < 2 * N && P.boxed;
+        sh.lb[i] = bx ? P.lb[i] : -UNBOXED_BOUND;
+        sh.ub[i] = bx ? P.ub[i] : UNBOXED_BOUND;
     }
     for (int i = threadIdx.x; i < 60; i += blockDim.x) {
         const double v = P.s_mats[i];   // Q 16, P 16, A 16, B 8, R 4
@@ -592,9 +636,10 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
     const bool act = W.act;
     const bool boxact = act && P.boxed;
     const int li = act ? lane : 0;
-    const double lb = boxact ? P.lb[li] : -UNBOXED_BOUND;
-    const double ub = boxact ? P.ub[li] : UNBOXED_BOUND;
-    const double bndabs = fmax(fabs(lb), fabs(ub));
+    // lb / ub are re-read from LDS at every use (fewer live registers across the loops)
+#define LB_ (sh.lb[lane])
+#define UB_ (sh.ub[lane])
+#define BNDABS_ fmax(fabs(LB_), fabs(UB_))
     const int p = P.p;
     const int m_rows = p + (P.boxed ? 2 * NV : 0);
     const double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
@@ -626,7 +671,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
 #pragma unroll
             for (int k = 0; k < NX; ++k) q += P.hq[li * NX + k] * (xv[k] - xr[k]);
         }
-        double bn = boxact ? bndabs : 0.0;
+        double bn = boxact ? BNDABS_ : 0.0;
 #pragma unroll
         for (int s = 0; s < RS; ++s) {
             double v = 0.0;
@@ -639,9 +684,9 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
             wv.w[s * 64 + lane] = v;
             bn = fmax(bn, fabs(v));
         }
-        double u = boxact ? fmin(fmax(0.0, lb), ub) : 0.0;
-        double su = boxact ? fmax(ub - u, 1.0) : 1.0;
-        double sl = boxact ? fmax(u - lb, 1.0) : 1.0;
+        double u = boxact ? fmin(fmax(0.0, LB_), UB_) : 0.0;
+        double su = boxact ? fmax(UB_ - u, 1.0) : 1.0;
+        double sl = boxact ? fmax(u - LB_, 1.0) : 1.0;
         double zu = boxact ? 1.0 : 0.0, zl = zu;
         double s_[RS], z_[RS];
         {
@@ -662,7 +707,6 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
         double M[NV];
         PT_DECL
         for (;;) {
-            double rp[RS];
             double gtz, rd, rpu, rpl, mu;
             bool res_ok;
             {
@@ -677,13 +721,14 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                 double rpn = 0.0, musum = 0.0, gun = 0.0;
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
-                    rp[s] = W.rv[s] ? gu[s] + s_[s] - wv.w[s * 64 + lane] : 0.0;
-                    rpn = fmax(rpn, fabs(rp[s]));
+                    const double rps = W.rv[s] ? gu[s] + s_[s] - wv.w[s * 64 + lane] : 0.0;
+                    wv.rp[s * 64 + lane] = rps;
+                    rpn = fmax(rpn, fabs(rps));
                     gun = fmax(gun, fabs(gu[s]));
                     musum += s_[s] * z_[s];
                 }
-                rpu = boxact ? u + su - ub : 0.0;
-                rpl = boxact ? -u + sl + lb : 0.0;
+                rpu = boxact ? u + su - UB_ : 0.0;
+                rpl = boxact ? -u + sl + LB_ : 0.0;
                 rpn = fmax(rpn, fmax(fabs(rpu), fabs(rpl)));
                 musum += boxact ? su * zu + sl * zl : 0.0;
                 const double gz = gtz + (boxact ? zu - zl : 0.0);
@@ -710,8 +755,8 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                         wz += wsv * z_[s];
                         wzabs += fabs(wsv) * z_[s];
                     }
-                    const double lo = act ? fmin(gtz * lb, gtz * ub) : 0.0;
-                    const double sc = act ? fabs(gtz) * bndabs : 0.0;
+                    const double lo = act ? fmin(gtz * LB_, gtz * UB_) : 0.0;
+                    const double sc = act ? fabs(gtz) * BNDABS_ : 0.0;
                     const double lo_w = wave_sum(lo), wz_w = wave_sum(wz), sc_w = wave_sum(sc + wzabs);
                     if (lo_w - wz_w > 1e-12 * sc_w) { status = CARMPC_PRIMAL_INFEASIBLE; break; }
                 }
@@ -726,8 +771,9 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
             PT_MARK(1);
             W.build_M(M, polish ? dbu + dbl : (boxact ? zu * frcp(su) + zl * frcp(sl) : 0.0));
             PT_MARK(2);
-            const double inv_ii = kLdsChol ? cholesky_lds<NV>(M, lane, wv.bvec) : cholesky<NV>(M, lane);
-            const double inv2 = inv_ii * inv_ii;
+            const double inv2 = kChol == 2   ? cholesky_lds<NV>(M, lane, wv.bvec)
+                                 : kChol == 1 ? cholesky_lds_sqrt<NV>(M, lane, wv.bvec)
+                                              : cholesky<NV>(M, lane);
             PT_MARK(3);
             // row temporaries: ra = dS | y_g ; rb = dZ | ry_g ; (LDS) pa = dS_aff dZ_aff
             double ra[RS], rb[RS];
@@ -750,8 +796,8 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                     }
                     W.build_lam(t, true, wv.lam);
                     const double hg = W.adjoint(wv.lam);
-                    ryu = dbu != 0.0 ? ub - v0 : 0.0;
-                    ryl = dbl != 0.0 ? -lb + v0 : 0.0;
+                    ryu = dbu != 0.0 ? UB_ - v0 : 0.0;
+                    ryl = dbl != 0.0 ? -LB_ + v0 : 0.0;
                     rhs = act ? -q - (hg + rx) - v1 + v2 + dbu * ryu - dbl * ryl : 0.0;
                 } else if (k < 2) {
                     double t[RS];
@@ -759,7 +805,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                     for (int s = 0; s < RS; ++s) {
                         const double rc = s_[s] * z_[s] + (k == 1 ? wv.pa[s * 64 + lane] : 0.0) -
                                           (k == 1 && W.rv[s] ? sigma_mu : 0.0);
-                        t[s] = W.rv[s] ? (rc - z_[s] * rp[s]) * frcp(s_[s]) : 0.0;
+                        t[s] = W.rv[s] ? (rc - z_[s] * wv.rp[s * 64 + lane]) * frcp(s_[s]) : 0.0;
                     }
                     const double rcu = !boxact ? 0.0 : su * zu + pua - (k == 1 ? sigma_mu : 0.0);
                     const double rcl = !boxact ? 0.0 : sl * zl + pla - (k == 1 ? sigma_mu : 0.0);
@@ -791,7 +837,7 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
                     for (int s = 0; s < RS; ++s) {
                         const double rc = s_[s] * z_[s] + (k == 1 ? wv.pa[s * 64 + lane] : 0.0) -
                                           (k == 1 && W.rv[s] ? sigma_mu : 0.0);
-                        ra[s] = W.rv[s] ? -rp[s] - gs[s] : 0.0;
+                        ra[s] = W.rv[s] ? -wv.rp[s * 64 + lane] - gs[s] : 0.0;
                         rb[s] = W.rv[s] ? (-rc - z_[s] * ra[s]) * frcp(s_[s]) : 0.0;
                     }
                     const double rcu = !boxact ? 0.0 : su * zu + pua - (k == 1 ? sigma_mu : 0.0);
@@ -833,8 +879,8 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
             if (polish) {
                 double gx[RS];
                 W.gmul(act ? v0 : 0.0, gx);
-                double viol = boxact ? fmax(v0 - ub, lb - v0) : -INFINITY;
-                double wsc = boxact ? bndabs : 0.0, ysc = fmax(fabs(v1), fabs(v2)), ymin = fmin(v1, v2);
+                double viol = boxact ? fmax(v0 - UB_, LB_ - v0) : -INFINITY;
+                double wsc = boxact ? BNDABS_ : 0.0, ysc = fmax(fabs(v1), fabs(v2)), ymin = fmin(v1, v2);
                 // active opposite pairs form an equality: exempt from the sign test (oracle/qp.py)
                 bool paired[RS];
 #pragma unroll
@@ -893,6 +939,10 @@ __global__ void __launch_bounds__(512) ipm_staged_kernel(DevProblem P, int64_t b
     }
 }
 
+#undef LB_
+#undef UB_
+#undef BNDABS_
+
 // ---------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------
@@ -902,23 +952,23 @@ namespace {
 #endif
 constexpr int kStagedNs[] = {CARMPC_STAGED_NS};
 
-template <int N, int RS, bool kLdsChol>
+template <int N, int RS, int kChol, int kWPB>
 hipError_t launch_t(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
                     int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
-    auto kern = ipm_staged_kernel<N, RS, kLdsChol>;
+    auto kern = ipm_staged_kernel<N, RS, kChol, kWPB>;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 512, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kWPB * 64, 0);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    int64_t want = (batch + 7) / 8;
+    int64_t want = (batch + kWPB - 1) / kWPB;
     int64_t grid = (int64_t)cus * per_cu;
     if (want < grid) grid = want;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), 0, stream, P, batch, x0, xref, u_out, ld_u, status,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u, status,
                        iters, s);
     return hipGetLastError();
 }
@@ -926,23 +976,22 @@ hipError_t launch_t(const DevProblem& P, int64_t batch, const double* x0, const 
 template <int N>
 hipError_t launch_rs(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
                      int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
-    // kernel id 4: readlane-broadcast Cholesky (A/B reference); otherwise LDS broadcast
-    if (s.kernel == 4) {
-        switch (P.srs) {
-            case 1: return launch_t<N, 1, false>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-            case 2: return launch_t<N, 2, false>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-            case 3: return launch_t<N, 3, false>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-            case 4: return launch_t<N, 4, false>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-            default: return hipErrorInvalidValue;
-        }
+    // default (2): LDS-broadcast Cholesky with square roots, 8 waves per workgroup (fastest
+    // measured); A/B variants: 4 readlane-broadcast Cholesky, 5 four waves per
+    // workgroup (one wave per SIMD, 512 registers), 6 square-root-free LDL'.
+#define CARMPC_RS_SWITCH(LDS, WPB)                                                                    \
+    switch (P.srs) {                                                                                  \
+        case 1: return launch_t<N, 1, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
+        case 2: return launch_t<N, 2, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
+        case 3: return launch_t<N, 3, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
+        case 4: return launch_t<N, 4, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
+        default: return hipErrorInvalidValue;                                                         \
     }
-    switch (P.srs) {
-        case 1: return launch_t<N, 1, true>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-        case 2: return launch_t<N, 2, true>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-        case 3: return launch_t<N, 3, true>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-        case 4: return launch_t<N, 4, true>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
-        default: return hipErrorInvalidValue;
-    }
+    if (s.kernel == 4) { CARMPC_RS_SWITCH(0, 8) }
+    if (s.kernel == 5) { CARMPC_RS_SWITCH(1, 4) }
+    if (s.kernel == 6) { CARMPC_RS_SWITCH(2, 8) }
+    CARMPC_RS_SWITCH(1, 8)
+#undef CARMPC_RS_SWITCH
 }
 }  // namespace
 

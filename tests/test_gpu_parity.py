@@ -58,7 +58,7 @@ def test_assembly_kernel_matches_oracle(gpu_available, name, N):
     np.testing.assert_allclose(m["S"], golden["S"], rtol=0, atol=1e-13)
 
 
-KERNELS = [1, 2, 4]   # dense, staged (LDS Cholesky), staged (readlane Cholesky): carmpc_settings.kernel
+KERNELS = [1, 2, 4, 5, 6]   # carmpc_settings.kernel: dense; staged (default); staged A/B variants
 
 
 def _settings(kernel):
