@@ -12,7 +12,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libcarmpc.so")
-SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip"]
+SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip"]
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I" + os.path.join(REPO, "include")]
@@ -28,7 +28,8 @@ def _hipcc():
 def _stale(obj, src):
     if not os.path.exists(obj):
         return True
-    deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(REPO, "include", "carmpc.h")]
+    deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h"),
+            os.path.join(REPO, "include", "carmpc.h")]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 

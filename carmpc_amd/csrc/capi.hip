@@ -240,10 +240,90 @@ int stage_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vecto
     return CARMPC_OK;
 }
 
+// Row layout of the grouped Riccati kernel (ipm_riccati.hip): 16 lanes per QP; lane j owns
+// stage j+1 (segment 0) and stage j+17 (segment 1), 8 row slots each.  Rows of stage k < N go
+// to the owner's segment; stage-N rows (terminal set + state rows on x_N) fill the owner of
+// N first, then the "overflow" segments whose stage number exceeds N (least-filled first).
+// Slot e = (seg*8 + s)*16 + j.  Returns ok=false (kernel unavailable) when it does not fit.
+int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vector<int32_t>& partner, bool* ok) {
+    *ok = false;
+    DevProblem& D = P->dev;
+    const int N = D.N;
+    if (D.nu != 2 || !riccati_supported_N(N) || D.n != 2 * N || N > 32) return CARMPC_OK;
+    std::vector<int32_t> stage(D.p);
+    std::vector<double> coefp((size_t)D.p * NX), w0p(D.p), Ep((size_t)D.p * NX);
+    if (D.p > 0) {
+        HIP_TRY(hipMemcpy(stage.data(), D.row_stage, sizeof(int32_t) * stage.size(), hipMemcpyDeviceToHost), "readback stage");
+        HIP_TRY(hipMemcpy(coefp.data(), D.row_coef, sizeof(double) * coefp.size(), hipMemcpyDeviceToHost), "readback coef");
+        HIP_TRY(hipMemcpy(w0p.data(), D.w0, sizeof(double) * w0p.size(), hipMemcpyDeviceToHost), "readback w0");
+        HIP_TRY(hipMemcpy(Ep.data(), D.E, sizeof(double) * Ep.size(), hipMemcpyDeviceToHost), "readback E");
+    }
+    int cnt[2][16] = {};
+    std::vector<int32_t> slot_of(D.p, -1);
+    for (int r = 0; r < D.p; ++r) {
+        const int k = stage[r];
+        if (k < 1 || k > N) return CARMPC_OK;
+        int sg = (k - 1) / 16, j = (k - 1) % 16;
+        if (cnt[sg][j] >= kRicSeg) {
+            if (k != N) return CARMPC_OK;
+            int best = -1;
+            for (int s2 = 0; s2 < 2; ++s2)
+                for (int j2 = 0; j2 < 16; ++j2)
+                    if (j2 + 1 + 16 * s2 > N && cnt[s2][j2] < kRicSeg && (best < 0 || cnt[s2][j2] < cnt[best / 16][best % 16]))
+                        best = s2 * 16 + j2;
+            if (best < 0) return CARMPC_OK;
+            sg = best / 16;
+            j = best % 16;
+        }
+        slot_of[r] = ((sg * kRicSeg + cnt[sg][j]) * 16) + j;
+        ++cnt[sg][j];
+    }
+    const int ns = kRicSlots * kRicLanes;
+    std::vector<double> sc((size_t)ns * NX, 0.0), sw(ns, 0.0), sE((size_t)ns * NX, 0.0);
+    std::vector<int32_t> sv(ns, 0), sp(ns, -1);
+    bool any_pair = false;
+    for (int r = 0; r < D.p; ++r) {
+        const int e = slot_of[r];
+        sv[e] = 1;
+        sw[e] = w0p[r];
+        for (int a = 0; a < NX; ++a) { sc[(size_t)e * NX + a] = coefp[(size_t)r * NX + a]; sE[(size_t)e * NX + a] = Ep[(size_t)r * NX + a]; }
+        if (!partner.empty() && partner[r] >= 0) {
+            sp[e] = slot_of[partner[r]];
+            any_pair = true;
+        }
+    }
+    double *dsc, *dsw, *dsE;
+    int32_t* dsv;
+    HIP_TRY(upload(P, &dsc, sc.data(), sc.size()), "upload r_coef");
+    HIP_TRY(upload(P, &dsw, sw.data(), sw.size()), "upload r_w0");
+    HIP_TRY(upload(P, &dsE, sE.data(), sE.size()), "upload r_E");
+    HIP_TRY(upload(P, &dsv, sv.data(), sv.size()), "upload r_valid");
+    D.r_coef = dsc; D.r_w0 = dsw; D.r_E = dsE; D.r_valid = dsv; D.r_partner = nullptr;
+    if (any_pair) {
+        int32_t* dsp = nullptr;
+        HIP_TRY(upload(P, &dsp, sp.data(), sp.size()), "upload r_partner");
+        D.r_partner = dsp;
+    }
+    StageMats& M = D.mats;
+    for (int i = 0; i < 4; ++i)
+        for (int jj = 0; jj < 4; ++jj) {
+            M.A[i * 4 + jj] = d->A[i * 4 + jj];
+            M.Q[i * 4 + jj] = 0.5 * (d->Q[i * 4 + jj] + d->Q[jj * 4 + i]);
+            M.P[i * 4 + jj] = 0.5 * (d->P[i * 4 + jj] + d->P[jj * 4 + i]);
+        }
+    for (int i = 0; i < 8; ++i) M.B[i] = d->B[i];
+    for (int i = 0; i < 2; ++i)
+        for (int jj = 0; jj < 2; ++jj) M.R[i * 2 + jj] = 0.5 * (d->R[i * 2 + jj] + d->R[jj * 2 + i]);
+    D.ric = 1;
+    *ok = true;
+    return CARMPC_OK;
+}
+
 // Kernel choice for one launch (settings.kernel).
 hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, const double* xref, double* u_out,
                         int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
+    if (s.kernel == 7) return launch_riccati(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     const bool staged = (s.kernel >= 4 && s.kernel <= 6) || s.kernel == 2 || (s.kernel == 0 && D.staged);
     if (staged) return launch_staged(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     return launch_dense(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
@@ -394,6 +474,8 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     std::vector<int32_t> partner;
     if (rc == CARMPC_OK) rc = setup_pairs(P, partner);
     if (rc == CARMPC_OK) rc = stage_layout(P, d, qp, Phi, partner, &staged);
+    bool ric = false;
+    if (rc == CARMPC_OK) rc = riccati_layout(P, d, partner, &ric);
     if (rc != CARMPC_OK) {
         delete P;
         return rc;

@@ -14,6 +14,16 @@ constexpr double PRE_TOL = 1e-9;      // x0-only row tolerance
 constexpr double STEP_FRAC = 0.99;
 constexpr double ZERO_ROW = 1e-12;    // relative row-norm threshold for x0-only rows
 
+// Small stage matrices by value (symmetrised Q, P, R): kernel arguments, so the grouped
+// kernel reads them through the scalar cache.
+struct StageMats {
+    double A[16];   // [a][b]
+    double B[8];    // [a][c]
+    double Q[16];   // Qbar_k, k < N
+    double P[16];   // Qbar_N (DARE terminal cost)
+    double R[4];
+};
+
 // Everything a solve kernel reads, as device pointers.  Lives in the problem
 // handle; passed to kernels by value.
 struct DevProblem {
@@ -54,6 +64,15 @@ struct DevProblem {
     // terminal set, mpc.py:107-117); nullptr when the problem has none
     const int32_t* partner;   // p: packed index of the opposite row or -1 (dense kernel)
     const int32_t* s_partner; // srs*64: slot index of the opposite row or -1 (staged kernel)
+    // grouped Riccati layout (ipm_riccati.hip, capi.hip::riccati_layout): 16 lanes per QP,
+    // lane j owns stage j+1 (segment 0) and j+17 (segment 1); slot e = (seg*8 + s)*16 + j
+    int32_t ric;              // layout present
+    const double* r_coef;     // 256 x NX  normalised row coefficients c~ of each slot
+    const double* r_w0;       // 256
+    const double* r_E;        // 256 x NX
+    const int32_t* r_valid;   // 256
+    const int32_t* r_partner; // 256: slot of the opposite row or -1; nullptr when none
+    StageMats mats;
 };
 
 struct Settings {
@@ -105,6 +124,13 @@ hipError_t launch_dense(const DevProblem& P, int64_t batch, const double* x0, co
                         const Settings& s, hipStream_t stream, int* unsupported);
 bool dense_supported(int nv, int p, size_t* lds_bytes);
 int dense_pick_nv(int n);
+
+// Grouped stage-form (Riccati) kernel (ipm_riccati.hip).
+constexpr int kRicLanes = 16, kRicSeg = 8, kRicSlots = 2 * kRicSeg;
+bool riccati_supported_N(int N);
+hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref,
+                          double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
+                          const Settings& s, hipStream_t stream, int* unsupported);
 
 // Stage-structured kernel (ipm_staged.hip).
 constexpr int kStagedMaxRS = 4;

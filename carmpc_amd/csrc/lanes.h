@@ -1,0 +1,61 @@
+// lanes.h -- cross-lane and arithmetic primitives for gfx950 solve kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+namespace carmpc {
+namespace lanes {
+
+// DPP butterflies inside a 16-lane row: quad xor 1, quad xor 2, half-row mirror, row
+// mirror.  Both lanes of each pair combine the same two operands, so every lane of the
+// row ends with a bitwise-identical result (row-uniform decisions stay consistent).
+constexpr int DPP_QXOR1 = 0xB1, DPP_QXOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+struct OpSum { __device__ static double f(double a, double b) { return a + b; } };
+struct OpMax { __device__ static double f(double a, double b) { return fmax(a, b); } };
+struct OpMin { __device__ static double f(double a, double b) { return fmin(a, b); } };
+
+// reduction over each 16-lane row (one QP group), result in every lane of the row
+template <class Op>
+__device__ __forceinline__ double row_reduce(double v) {
+    v = Op::f(v, dpp_d<DPP_QXOR1>(v));
+    v = Op::f(v, dpp_d<DPP_QXOR2>(v));
+    v = Op::f(v, dpp_d<DPP_HMIRROR>(v));
+    return Op::f(v, dpp_d<DPP_MIRROR>(v));
+}
+__device__ __forceinline__ double row_sum(double v) { return row_reduce<OpSum>(v); }
+__device__ __forceinline__ double row_max(double v) { return row_reduce<OpMax>(v); }
+__device__ __forceinline__ double row_min(double v) { return row_reduce<OpMin>(v); }
+
+// Reciprocal / reciprocal square root: hardware approximation + two Newton steps.
+__device__ __forceinline__ double frcp(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return fma(fma(-b, r, 1.0), r, r);
+}
+__device__ __forceinline__ double frsq(double a) {
+    double r = __builtin_amdgcn_rsq(a);
+    const double h = 0.5 * a;
+    r = r * fma(-h * r, r, 1.5);
+    return r * fma(-h * r, r, 1.5);
+}
+// step to the boundary along dv (inf when dv >= 0)
+__device__ __forceinline__ double ratio(double v, double dv) {
+    const double r = -v * __builtin_amdgcn_rcp(dv);
+    return dv < 0.0 ? r : INFINITY;
+}
+// index of the symmetric 4x4 entry (a <= b) in the packed 10-vector
+__host__ __device__ constexpr int sym10(int a, int b) {
+    return a <= b ? a * 4 - a * (a - 1) / 2 + (b - a) : b * 4 - b * (b - 1) / 2 + (a - b);
+}
+
+}  // namespace lanes
+}  // namespace carmpc
