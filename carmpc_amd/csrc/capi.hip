@@ -314,7 +314,21 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
     for (int i = 0; i < 8; ++i) M.B[i] = d->B[i];
     for (int i = 0; i < 2; ++i)
         for (int jj = 0; jj < 2; ++jj) M.R[i * 2 + jj] = 0.5 * (d->R[i * 2 + jj] + d->R[jj * 2 + i]);
-    D.ric = 1;
+    // structural zeros of the bicycle model (ipm_riccati.hip::BicycleModel): exact zeros outside
+    // the masks and a unit diagonal of A select the sparse instantiation
+    auto zero_outside = [](const double* X, int rows, int cols, const int* keep, int nkeep) {
+        for (int i = 0; i < rows * cols; ++i) {
+            bool k = false;
+            for (int t = 0; t < nkeep; ++t) k = k || keep[t] == i;
+            if (!k && X[i] != 0.0) return false;
+        }
+        return true;
+    };
+    const int keepA[] = {0, 2, 3, 5, 6, 7, 10, 11, 15}, keepB[] = {5, 6}, keepQ[] = {0, 5, 10, 15}, keepR[] = {0, 3};
+    const bool bike = zero_outside(M.A, 4, 4, keepA, 9) && M.A[0] == 1.0 && M.A[5] == 1.0 && M.A[10] == 1.0 &&
+                      M.A[15] == 1.0 && zero_outside(M.B, 4, 2, keepB, 2) && zero_outside(M.Q, 4, 4, keepQ, 4) &&
+                      zero_outside(M.R, 2, 2, keepR, 2);
+    D.ric = bike ? 2 : 1;
     *ok = true;
     return CARMPC_OK;
 }

@@ -53,16 +53,64 @@ struct RicShared {
     int32_t partner[RS * G16];
     double lb[64], ub[64];
 };
+// per-input state of the owned inputs, one row of 12 fields x 2 components per input pair t
+// (row N: dummy row written by lanes whose segment owns no input)
+enum { F_U = 0, F_Q, F_SU, F_SL, F_ZU, F_ZL, F_RD, F_E1, F_E2, F_E3, F_E4, F_VX, F_COUNT };
 template <int N>
 struct RicWave {
-    double rec[4][N * REC];
+    // stage records of the 4 groups; the polish verification scratch [RS][64] aliases them
+    double recbuf[4 * N * REC > RS * 64 ? 4 * N * REC : RS * 64];
     double w[RS][64];         // w = w0 - E x0 per (slot, lane)
-    double scr[RS][64];       // polish verification scratch
+    double vbox[4][N + 1][F_COUNT * 2];
 };
 
 __device__ __forceinline__ void wb() { __builtin_amdgcn_wave_barrier(); }
 
-template <int N, int WPB>
+// Compile-time sparsity of the stage matrices: entries outside a mask are exactly zero and,
+// with AUNIT, diag(A) == 1 exactly (verified on the host, capi.hip::riccati_layout), so the
+// unrolled products skip them.  DenseModel is the general fallback.
+constexpr unsigned bit4(int a, int b) { return 1u << (a * 4 + b); }
+constexpr unsigned bit2(int a, int b) { return 1u << (a * 2 + b); }
+struct DenseModel {
+    static constexpr unsigned A = 0xFFFFu, B = 0xFFu, Q = 0xFFFFu, R = 0xFu;
+    static constexpr bool AUNIT = false;
+};
+// kinematic bicycle linearised and discretised as in mpc.py:128-180: A = I + dt A_lin with
+// A_lin nonzero only in rows 0-1 (columns 2-3) and entry (2,3); B = dt B_lin with B_lin[2][1],
+// B_lin[3][0]; Q, R diagonal (configuration.py:19-21).
+struct BicycleModel {
+    static constexpr unsigned A = bit4(0, 0) | bit4(0, 2) | bit4(0, 3) | bit4(1, 1) | bit4(1, 2) | bit4(1, 3) |
+                                  bit4(2, 2) | bit4(2, 3) | bit4(3, 3);
+    static constexpr unsigned B = bit2(2, 1) | bit2(3, 0);
+    static constexpr unsigned Q = bit4(0, 0) | bit4(1, 1) | bit4(2, 2) | bit4(3, 3);
+    static constexpr unsigned R = bit2(0, 0) | bit2(1, 1);
+    static constexpr bool AUNIT = true;
+};
+template <class SP>
+struct Mt {
+    const StageMats& m;
+    // acc + X[a][b] * x, skipping structural zeros (indices are unrolled constants)
+    __device__ __forceinline__ double A_(int a, int b, double x, double acc) const {
+        if (!((SP::A >> (a * 4 + b)) & 1u)) return acc;
+        if (SP::AUNIT && a == b) return acc + x;
+        return fma(m.A[a * 4 + b], x, acc);
+    }
+    __device__ __forceinline__ double B_(int a, int c, double x, double acc) const {
+        return ((SP::B >> (a * 2 + c)) & 1u) ? fma(m.B[a * 2 + c], x, acc) : acc;
+    }
+    __device__ __forceinline__ double Q_(int a, int b, double x, double acc) const {
+        return ((SP::Q >> (a * 4 + b)) & 1u) ? fma(m.Q[a * 4 + b], x, acc) : acc;
+    }
+    __device__ __forceinline__ double R_(int c, int d, double x, double acc) const {
+        return ((SP::R >> (c * 2 + d)) & 1u) ? fma(m.R[c * 2 + d], x, acc) : acc;
+    }
+    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : 0.0; }
+    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : 0.0; }
+    // (R v)_c
+    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, 0.0)); }
+};
+
+template <int N, int WPB, class SP>
 __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int64_t batch, const double* __restrict__ x0,
                                                                const double* __restrict__ xref, double* __restrict__ u_out,
                                                                int64_t ld_u, int32_t* __restrict__ status_out,
@@ -70,6 +118,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
     __shared__ __attribute__((aligned(16))) RicWave<N> wscr[WPB];
     const StageMats& MT = P.mats;
+    const Mt<SP> M{P.mats};
     for (int i = threadIdx.x; i < RS * G16; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.r_coef[i * 4 + 0], P.r_coef[i * 4 + 1]);
         sh.cf23[i] = make_double2(P.r_coef[i * 4 + 2], P.r_coef[i * 4 + 3]);
@@ -86,7 +135,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     const int wave = threadIdx.x >> 6;
     const int g = lane >> 4, j = lane & 15;
     RicWave<N>& wv = wscr[wave];
-    double* rec = wv.rec[g];
+    double* rec = wv.recbuf + g * (N * REC);
+    double(*scr)[64] = reinterpret_cast<double(*)[64]>(wv.recbuf);
     const bool boxed = P.boxed != 0;
     // segment stages: seg 0 -> j+1, seg 1 -> j+17 (overflow segments -> stage N)
     int kseg[2];
@@ -98,6 +148,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         kseg[sg] = k <= N ? k : N;
         isN[sg] = kseg[sg] == N;
     }
+    double* vb[2];
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) vb[sg] = &wv.vbox[g][own[sg] ? kseg[sg] - 1 : N][0];
+#define BX(F, sg, c) vb[sg][(F) * 2 + (c)]
     bool rv[RS];
 #pragma unroll
     for (int s = 0; s < RS; ++s) rv[s] = P.r_valid[s * G16 + j] != 0;
@@ -140,10 +194,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto add_qbar = [&](bool termN, const double (&v)[4], double (&y)[4], double sgn) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            double acc = 0.0;
+            double accp = 0.0, accq = 0.0;
 #pragma unroll
-            for (int b = 0; b < 4; ++b) acc = fma(termN ? MT.P[a * 4 + b] : MT.Q[a * 4 + b], v[b], acc);
-            y[a] = fma(sgn, acc, y[a]);
+            for (int b = 0; b < 4; ++b) {
+                accp = fma(MT.P[a * 4 + b], v[b], accp);
+                accq = M.Q_(a, b, v[b], accq);
+            }
+            y[a] = fma(sgn, termN ? accp : accq, y[a]);
         }
     };
     // sum the stage-N partials of the 16 lanes; owners write b^x (plus Qbar term) of their stages
@@ -172,7 +229,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         wb();
         double pv[4];
         rd4((N - 1) * REC + O_BX, pv);
-#pragma unroll
+#pragma unroll 1
         for (int t = N - 1; t >= 0; --t) {
             const int r = t * REC;
             double bu0, bu1, il00, l10, il11, dummy;
@@ -184,8 +241,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double g0 = bu0, g1 = bu1;
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                g0 = fma(MT.B[a * 2 + 0], pv[a], g0);
-                g1 = fma(MT.B[a * 2 + 1], pv[a], g1);
+                g0 = M.B_(a, 0, pv[a], g0);
+                g1 = M.B_(a, 1, pv[a], g1);
             }
             const double y0 = g0 * il00;
             const double y1 = fma(-l10, y0, g1) * il11;
@@ -200,7 +257,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 for (int a = 0; a < 4; ++a) {
                     double acc = bx[a];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) acc = fma(MT.A[c * 4 + a], pv[c], acc);
+                    for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
                     acc = fma(-K[a], g0, acc);
                     np[a] = fma(-K[4 + a], g1, acc);
                 }
@@ -214,7 +271,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto forward = [&]() {
         wb();
         double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
+#pragma unroll 1
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             double k0, k1;
@@ -230,10 +287,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double ny[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                double acc = MT.B[a * 2] * v0;
-                acc = fma(MT.B[a * 2 + 1], v1, acc);
+                double acc = M.B_(a, 0, v0, 0.0);
+                acc = M.B_(a, 1, v1, acc);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc = fma(MT.A[a * 4 + c], y[c], acc);
+                for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
                 ny[a] = acc;
             }
 #pragma unroll
@@ -249,7 +306,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto rollout = [&]() {
         wb();
         double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
+#pragma unroll 1
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             double v0, v1;
@@ -257,10 +314,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double ny[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                double acc = MT.B[a * 2] * v0;
-                acc = fma(MT.B[a * 2 + 1], v1, acc);
+                double acc = M.B_(a, 0, v0, 0.0);
+                acc = M.B_(a, 1, v1, acc);
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc = fma(MT.A[a * 4 + c], y[c], acc);
+                for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
                 ny[a] = acc;
             }
 #pragma unroll
@@ -291,42 +348,33 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double db0, db1, bu0, bu1;
             rd2(r + O_DB, db0, db1);
             rd2(r + O_BU, bu0, bu1);
-            // PB = P B (4x2), PA = P A (4x4)
-            double PB[4][2], PA[4][4];
+            // PB = P B (4x2); Re = R + diag(Db) + B'PB; F = B'PA = (PB)'A
+            double PB[4][2];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) {
+            for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     double acc = 0.0;
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) acc = fma(Pm[sym10(a, b)], MT.B[b * 2 + c], acc);
+                    for (int b = 0; b < 4; ++b) acc = M.B_(b, c, Pm[sym10(a, b)], acc);
                     PB[a][c] = acc;
                 }
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) acc = fma(Pm[sym10(a, b)], MT.A[b * 4 + m], acc);
-                    PA[a][m] = acc;
-                }
-            }
-            // Re = R + diag(Db) + B'PB ; F = B'PA
-            double re00 = MT.R[0] + db0, re10 = MT.R[2], re11 = MT.R[3] + db1;
+            double re00 = M.Rv(0, 0) + db0, re10 = M.Rv(1, 0), re11 = M.Rv(1, 1) + db1;
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                re00 = fma(MT.B[a * 2 + 0], PB[a][0], re00);
-                re10 = fma(MT.B[a * 2 + 1], PB[a][0], re10);
-                re11 = fma(MT.B[a * 2 + 1], PB[a][1], re11);
+                re00 = M.B_(a, 0, PB[a][0], re00);
+                re10 = M.B_(a, 1, PB[a][0], re10);
+                re11 = M.B_(a, 1, PB[a][1], re11);
             }
             double F[2][4];
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
+                for (int mm = 0; mm < 4; ++mm) {
                     double acc = 0.0;
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) acc = fma(MT.B[a * 2 + c], PA[a][m], acc);
-                    F[c][m] = acc;
+                    for (int a = 0; a < 4; ++a) acc = M.A_(a, mm, PB[a][c], acc);
+                    F[c][mm] = acc;
                 }
             // guarded 2x2 Cholesky (non-positive pivot -> 1e128, as qp._chol_guarded)
             double p0 = re00;
@@ -347,8 +395,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double g0 = bu0, g1 = bu1;
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                g0 = fma(MT.B[a * 2 + 0], pv[a], g0);
-                g1 = fma(MT.B[a * 2 + 1], pv[a], g1);
+                g0 = M.B_(a, 0, pv[a], g0);
+                g1 = M.B_(a, 1, pv[a], g1);
             }
             const double y0 = g0 * il00;
             const double y1 = fma(-l10, y0, g1) * il11;
@@ -367,23 +415,35 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                 for (int e = 0; e < 5; ++e) rd2(r - REC + 2 * e, Wt[2 * e], Wt[2 * e + 1]);
                 rd4(r - REC + O_BX, bx);
-                // P_t = Qbar_t + W_t + A'PA - F'K  (upper triangle)
+                // P_t = Qbar_t + W_t + A'PA - F'K  (upper triangle), PA one column at a time
+                double Pn[10];
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+                for (int b = 0; b < 4; ++b) {
+                    double col[4];
 #pragma unroll
-                    for (int b = a; b < 4; ++b) {
-                        double acc = MT.Q[a * 4 + b] + Wt[sym10(a, b)];
+                    for (int c = 0; c < 4; ++c) {
+                        double acc = 0.0;
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) acc = fma(MT.A[c * 4 + a], PA[c][b], acc);
-                        acc = fma(-F[0][a], K[0][b], acc);
-                        Pm[sym10(a, b)] = fma(-F[1][a], K[1][b], acc);
+                        for (int d = 0; d < 4; ++d) acc = M.A_(d, b, Pm[sym10(c, d)], acc);
+                        col[c] = acc;
                     }
+#pragma unroll
+                    for (int a = 0; a <= b; ++a) {
+                        double acc = M.Qv(a, b) + Wt[sym10(a, b)];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) acc = M.A_(c, a, col[c], acc);
+                        acc = fma(-F[0][a], K[0][b], acc);
+                        Pn[sym10(a, b)] = fma(-F[1][a], K[1][b], acc);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 10; ++e) Pm[e] = Pn[e];
                 double np[4];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     double acc = bx[a];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) acc = fma(MT.A[c * 4 + a], pv[c], acc);
+                    for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
                     acc = fma(-K[0][a], g0, acc);
                     np[a] = fma(-K[1][a], g1, acc);
                 }
@@ -394,20 +454,46 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         wb();
     };
 
-    const int64_t per_wave = 4;
-    const int64_t stride = (int64_t)gridDim.x * WPB * per_wave;
-    for (int64_t base = ((int64_t)blockIdx.x * WPB + wave) * per_wave; base < batch; base += stride) {
-        const int64_t inst = base + g;
-        bool active = inst < batch;
-        const int64_t ii = active ? inst : 0;
-        double xv0[NX], xr[NX];
+    // Each group walks its own instance sequence (inst, inst + stride, ...) and starts the
+    // next instance at the first trip after finishing one, so the 4 groups of a wave never
+    // wait for the slowest instance (infeasible ones stop after a few iterations).
+    const int64_t stride = (int64_t)gridDim.x * WPB * 4;
+    int64_t inst = ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
+    bool live = inst < batch;   // the group has an instance to work on
+    bool fresh = true;          // ... that still needs its initial point
+    double s_[RS], z_[RS], ra[RS];
+    double xs[2][4];
+    double bnorm = 1.0, qnorm = 1.0;
+    int it = 0;
+    bool polish_failed = false;
+    // write the result of the current instance and move the group to its next one
+    auto finish = [&](int st, bool zero_u) {
 #pragma unroll
-        for (int k = 0; k < NX; ++k) {
-            xv0[k] = x0[ii * NX + k];
-            xr[k] = xref ? xref[ii * NX + k] : P.goal[k];
+        for (int sg = 0; sg < 2; ++sg)
+            if (own[sg]) {
+                const int t = kseg[sg] - 1;
+                u_out[inst * ld_u + 2 * t] = zero_u ? 0.0 : BX(F_U, sg, 0);
+                u_out[inst * ld_u + 2 * t + 1] = zero_u ? 0.0 : BX(F_U, sg, 1);
+            }
+        if (j == 0) {
+            status_out[inst] = st;
+            if (iters_out) iters_out[inst] = it;
         }
-        // x0-only rows (G_r = 0): preconditions
-        {
+        inst += stride;
+        live = inst < batch;
+        fresh = true;
+    };
+    while (__any(live)) {
+        bool active = live;
+        if (live && fresh) {
+            fresh = false;
+            double xv0[NX], xr[NX];
+#pragma unroll
+            for (int k = 0; k < NX; ++k) {
+                xv0[k] = x0[inst * NX + k];
+                xr[k] = xref ? xref[inst * NX + k] : P.goal[k];
+            }
+            // x0-only rows (G_r = 0): preconditions
             double bad = 0.0;
             for (int r = j; r < P.npre; r += G16) {
                 double v = P.pre_w0[r];
@@ -415,86 +501,80 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv0[k];
                 bad = v < -PRE_TOL ? 1.0 : bad;
             }
-            bad = row_max(bad);
-            if (active && bad > 0.0) {
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg)
-                    if (own[sg]) {
-                        const int t = kseg[sg] - 1;
-                        u_out[inst * ld_u + 2 * t] = 0.0;
-                        u_out[inst * ld_u + 2 * t + 1] = 0.0;
-                    }
-                if (j == 0) {
-                    status_out[inst] = CARMPC_PRIMAL_INFEASIBLE;
-                    if (iters_out) iters_out[inst] = 0;
-                }
+            it = 0;
+            polish_failed = false;
+            if (row_max(bad) > 0.0) {
+                finish(CARMPC_PRIMAL_INFEASIBLE, true);
                 active = false;
+            } else {
+                // per-slot w, q and box of the owned inputs, initial point
+                double bn = 0.0, qn = 0.0, u0n = 0.0;
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+                    double v = 0.0;
+                    if (rv[s]) {
+                        const int e = s * G16 + j;
+                        v = P.r_w0[e];
+#pragma unroll
+                        for (int k = 0; k < NX; ++k) v -= P.r_E[e * NX + k] * xv0[k];
+                    }
+                    wv.w[s][lane] = v;
+                    bn = fmax(bn, fabs(v));
+                }
+#pragma unroll
+                for (int sg = 0; sg < 2; ++sg) {
+                    const int t = kseg[sg] - 1;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int i = 2 * t + c;
+                        double q = 0.0;
+#pragma unroll
+                        for (int k = 0; k < NX; ++k) q = fma(P.hq[i * NX + k], xv0[k] - xr[k], q);
+                        const double lb = sh.lb[i], ub = sh.ub[i];
+                        const bool bx = own[sg] && boxed;
+                        const double u0 = bx ? fmin(fmax(0.0, lb), ub) : 0.0;
+                        BX(F_Q, sg, c) = own[sg] ? q : 0.0;
+                        BX(F_U, sg, c) = u0;
+                        BX(F_SU, sg, c) = bx ? fmax(ub - u0, 1.0) : 1.0;
+                        BX(F_SL, sg, c) = bx ? fmax(u0 - lb, 1.0) : 1.0;
+                        BX(F_ZU, sg, c) = bx ? 1.0 : 0.0;
+                        BX(F_ZL, sg, c) = bx ? 1.0 : 0.0;
+                        bn = bx ? fmax(bn, fmax(fabs(lb), fabs(ub))) : bn;
+                        qn = fmax(qn, own[sg] ? fabs(q) : 0.0);
+                        u0n = fmax(u0n, fabs(u0));
+                    }
+                }
+                // xs = S u0 (u0 = clip(0, lb, ub); zero whenever the box contains 0)
+                if (row_max(u0n) > 0.0) {
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg)
+                        if (own[sg]) wr2((kseg[sg] - 1) * REC + O_BU, BX(F_U, sg, 0), BX(F_U, sg, 1));
+                    rollout();
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg) rd4((kseg[sg] - 1) * REC + O_BX, xs[sg]);
+                } else {
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) xs[sg][a] = 0.0;
+                }
+#pragma unroll
+                for (int s = 0; s < RS; ++s) {
+                    const int sg = s / RSEG;
+                    double c[4];
+                    cf(s, c);
+                    s_[s] = rv[s] ? fmax(wv.w[s][lane] - dot4(c, xs[sg]), 1.0) : 1.0;
+                    z_[s] = rv[s] ? 1.0 : 0.0;
+                    ra[s] = 0.0;
+                }
+                bnorm = 1.0 + row_max(bn);
+                qnorm = 1.0 + row_max(qn);
             }
         }
-        // per-slot w, q and box of the owned inputs, initial point
-        double s_[RS], z_[RS], ra[RS], rb[RS];
-        double u_[2][2], q_[2][2], su[2][2], sl[2][2], zu[2][2], zl[2][2];
-        double xs[2][4];
-        double bn = 0.0, qn = 0.0;
-#pragma unroll
-        for (int s = 0; s < RS; ++s) {
-            double v = 0.0;
-            if (rv[s]) {
-                const int e = s * G16 + j;
-                v = P.r_w0[e];
-#pragma unroll
-                for (int k = 0; k < NX; ++k) v -= P.r_E[e * NX + k] * xv0[k];
-            }
-            wv.w[s][lane] = v;
-            bn = fmax(bn, fabs(v));
-        }
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) {
-            const int t = kseg[sg] - 1;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int i = 2 * t + c;
-                double q = 0.0;
-#pragma unroll
-                for (int k = 0; k < NX; ++k) q = fma(P.hq[i * NX + k], xv0[k] - xr[k], q);
-                const double lb = sh.lb[i], ub = sh.ub[i];
-                const bool bx = own[sg] && boxed;
-                q_[sg][c] = own[sg] ? q : 0.0;
-                u_[sg][c] = bx ? fmin(fmax(0.0, lb), ub) : 0.0;
-                su[sg][c] = bx ? fmax(ub - u_[sg][c], 1.0) : 1.0;
-                sl[sg][c] = bx ? fmax(u_[sg][c] - lb, 1.0) : 1.0;
-                zu[sg][c] = bx ? 1.0 : 0.0;
-                zl[sg][c] = bx ? 1.0 : 0.0;
-                bn = bx ? fmax(bn, fmax(fabs(lb), fabs(ub))) : bn;
-                qn = fmax(qn, fabs(q_[sg][c]));
-            }
-        }
-        // xs = S u0 (u0 = clip(0, lb, ub))
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg)
-            if (own[sg]) wr2((kseg[sg] - 1) * REC + O_BU, u_[sg][0], u_[sg][1]);
-        rollout();
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) rd4((kseg[sg] - 1) * REC + O_BX, xs[sg]);
-#pragma unroll
-        for (int s = 0; s < RS; ++s) {
-            const int sg = s / RSEG;
-            double c[4];
-            cf(s, c);
-            s_[s] = rv[s] ? fmax(wv.w[s][lane] - dot4(c, xs[sg]), 1.0) : 1.0;
-            z_[s] = rv[s] ? 1.0 : 0.0;
-            ra[s] = 0.0;
-            rb[s] = 0.0;
-        }
-        const double bnorm = 1.0 + row_max(bn);
-        const double qnorm = 1.0 + row_max(qn);
-
-        int status = CARMPC_MAX_ITER;
-        int it = 0;
-        bool polish_failed = false;
-        while (__any(active)) {
+        if (!__any(active)) continue;
+        {
             // ================= residuals (R1 + B1) =================
-            double rd_[2][2], mu = 0.0, rpn = 0.0, gun = 0.0, umax = 0.0, wz = 0.0, wzabs = 0.0;
+            double mu = 0.0, rpn = 0.0, gun = 0.0, umax = 0.0, wz = 0.0, wzabs = 0.0;
             double lo = 0.0, scf = 0.0;
             bool polish = false;
             if (active) {
@@ -525,11 +605,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     for (int c = 0; c < 2; ++c) {
                         const int i = 2 * (kseg[sg] - 1) + c;
                         if (own[sg] && boxed) {
-                            const double rpu = u_[sg][c] + su[sg][c] - sh.ub[i];
-                            const double rpl = -u_[sg][c] + sl[sg][c] + sh.lb[i];
+                            const double rpu = BX(F_U, sg, c) + BX(F_SU, sg, c) - sh.ub[i];
+                            const double rpl = -BX(F_U, sg, c) + BX(F_SL, sg, c) + sh.lb[i];
                             rpn = fmax(rpn, fmax(fabs(rpu), fabs(rpl)));
-                            musum = fma(su[sg][c], zu[sg][c], fma(sl[sg][c], zl[sg][c], musum));
-                            umax = fmax(umax, fabs(u_[sg][c]));
+                            musum = fma(BX(F_SU, sg, c), BX(F_ZU, sg, c), fma(BX(F_SL, sg, c), BX(F_ZL, sg, c), musum));
+                            umax = fmax(umax, fabs(BX(F_U, sg, c)));
                         }
                     }
                 // stage-N sum of lamZ, owners write lamZ_k [0..3], lamH_k = Qbar_k xs_k [4..7]
@@ -557,7 +637,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 wb();
                 {
                     double pz[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
+#pragma unroll 1
                     for (int t = N - 1; t >= 0; --t) {
                         const int r = t * REC;
                         double lzv[4], lhv[4];
@@ -569,8 +649,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             double az = lzv[a], ah = lhv[a];
 #pragma unroll
                             for (int c = 0; c < 4; ++c) {
-                                az = fma(MT.A[c * 4 + a], pz[c], az);
-                                ah = fma(MT.A[c * 4 + a], ph[c], ah);
+                                az = M.A_(c, a, pz[c], az);
+                                ah = M.A_(c, a, ph[c], ah);
                             }
                             nz[a] = az;
                             nh[a] = ah;
@@ -583,8 +663,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             for (int a = 0; a < 4; ++a) {
                                 pz[a] = nz[a];
                                 ph[a] = nh[a];
-                                az = fma(MT.B[a * 2 + c], nz[a], az);
-                                ah = fma(MT.B[a * 2 + c], nh[a], ah);
+                                az = M.B_(a, c, nz[a], az);
+                                ah = M.B_(a, c, nh[a], ah);
                             }
                             gz[c] = az;
                             hs[c] = ah;
@@ -610,10 +690,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     const double gzv[2] = {gz0, gz1}, hsv[2] = {hs0, hs1};
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const double hu = hsv[c] + fma(MT.R[c * 2], u_[sg][0], MT.R[c * 2 + 1] * u_[sg][1]);
-                        const double gzb = gzv[c] + (boxed ? zu[sg][c] - zl[sg][c] : 0.0);
-                        const double rd = hu + q_[sg][c] + gzb;
-                        rd_[sg][c] = own[sg] ? rd : 0.0;
+                        const double hu = hsv[c] + M.Rmul(c, BX(F_U, sg, 0), BX(F_U, sg, 1));
+                        const double gzb = gzv[c] + (boxed ? BX(F_ZU, sg, c) - BX(F_ZL, sg, c) : 0.0);
+                        const double rd = hu + BX(F_Q, sg, c) + gzb;
+                        BX(F_RD, sg, c) = own[sg] ? rd : 0.0;
                         if (own[sg]) {
                             rdn = fmax(rdn, fabs(rd));
                             hun = fmax(hun, fabs(hu));
@@ -640,31 +720,18 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     }
                 }
                 if (done >= 0) {
-                    status = done;
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-                        if (own[sg]) {
-                            const int t = kseg[sg] - 1;
-                            u_out[inst * ld_u + 2 * t] = u_[sg][0];
-                            u_out[inst * ld_u + 2 * t + 1] = u_[sg][1];
-                        }
-                    if (j == 0) {
-                        status_out[inst] = status;
-                        if (iters_out) iters_out[inst] = it;
-                    }
+                    finish(done, false);
                     active = false;
                     polish = false;
                 }
             }
             const bool any_polish = __any(polish);
-            if (!__any(active)) break;
+            if (!__any(active)) continue;
             // ================= factorization rows (R2) + first right-hand side =================
             // normal: d = z/s, predictor rhs; polish: d = 1/delta on the active set (s < z)
             // per owned input: normal e1..e4 = dsu, dzu, dsl, dzl of the direction, vx = du;
             // polish vx = x, e1 = yu, e2 = yl.  xvv: normal S du (corrector), polish S x.
-            double e1[2][2], e2[2][2], e3[2][2], e4[2][2], vx[2][2];
-            double xvv[2][4];
-            double pua[2][2], pla[2][2];
+            double xvv[2][4], dyA[2][4];
             double smu = 0.0;
             if (active) {
                 double Wa[2][10], acc[2][4];
@@ -683,10 +750,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     const double w = wv.w[s][lane];
                     double d, t;
                     if (polish) {
+                        // b^x = -(Qbar S x + sum (yg - d ryg) c) at x = 0, yg = 0: ryg = w on active rows
                         d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
-                        rb[s] = d != 0.0 ? w : 0.0;       // ryg of the first polish solve (x = 0)
-                        ra[s] = 0.0;                       // yg
-                        t = -(ra[s] - d * rb[s]);          // b^x = -(Qbar xv + sum (yg - d ryg) c)
+                        t = d != 0.0 ? d * w : 0.0;
                     } else {
                         d = rv[s] ? z_[s] * frcp(s_[s]) : 0.0;
                         const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - w : 0.0;
@@ -716,31 +782,22 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     for (int c = 0; c < 2; ++c) {
                         const int i = 2 * t + c;
                         const double lb = sh.lb[i], ub = sh.ub[i];
-                        vx[sg][c] = 0.0;
-                        e1[sg][c] = 0.0;
-                        e2[sg][c] = 0.0;
-                        e3[sg][c] = 0.0;
-                        e4[sg][c] = 0.0;
-                        pua[sg][c] = 0.0;
-                        pla[sg][c] = 0.0;
                         if (polish) {
-                            const double dbu = (boxed && su[sg][c] < zu[sg][c]) ? idl : 0.0;
-                            const double dbl = (boxed && sl[sg][c] < zl[sg][c]) ? idl : 0.0;
+                            const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
+                            const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
                             db[c] = dbu + dbl;
-                            bu[c] = -q_[sg][c] + dbu * ub + dbl * lb;
+                            bu[c] = -BX(F_Q, sg, c) + dbu * ub + dbl * lb;
                         } else if (boxed) {
-                            const double rpu = u_[sg][c] + su[sg][c] - ub;
-                            const double rpl = -u_[sg][c] + sl[sg][c] + lb;
-                            db[c] = zu[sg][c] * frcp(su[sg][c]) + zl[sg][c] * frcp(sl[sg][c]);
-                            bu[c] = -rd_[sg][c] + (su[sg][c] * zu[sg][c] - zu[sg][c] * rpu) * frcp(su[sg][c]) -
-                                    (sl[sg][c] * zl[sg][c] - zl[sg][c] * rpl) * frcp(sl[sg][c]);
+                            const double rpu = BX(F_U, sg, c) + BX(F_SU, sg, c) - ub;
+                            const double rpl = -BX(F_U, sg, c) + BX(F_SL, sg, c) + lb;
+                            db[c] = BX(F_ZU, sg, c) * frcp(BX(F_SU, sg, c)) + BX(F_ZL, sg, c) * frcp(BX(F_SL, sg, c));
+                            bu[c] = -BX(F_RD, sg, c) + (BX(F_SU, sg, c) * BX(F_ZU, sg, c) - BX(F_ZU, sg, c) * rpu) * frcp(BX(F_SU, sg, c)) -
+                                    (BX(F_SL, sg, c) * BX(F_ZL, sg, c) - BX(F_ZL, sg, c) * rpl) * frcp(BX(F_SL, sg, c));
                         } else {
                             db[c] = 0.0;
-                            bu[c] = -rd_[sg][c];
+                            bu[c] = -BX(F_RD, sg, c);
                         }
                     }
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) xvv[sg][a] = 0.0;
                     if (own[sg]) {
 #pragma unroll
                         for (int e = 0; e < 5; ++e)
@@ -752,9 +809,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 factor_and_back();
             }
             // ================= solves =================
-            const int nsolve = any_polish ? POLISH_REFINE + 1 : 3;
-#pragma unroll 1
-            for (int k = 0; k < nsolve; ++k) {
+            // fully unrolled: k is a constant in every branch below (precise register lifetimes)
+#pragma unroll
+            for (int k = 0; k < POLISH_REFINE + 1; ++k) {
+                if (k == 3 && !any_polish) break;
                 const bool run = active && (polish || k < 3);
                 if (k > 0 && run) back_linear();
                 if (run) forward();
@@ -774,7 +832,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         double c[4];
                         cf(s, c);
                         const double d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
-                        ra[s] = fma(d, dot4(c, dy[sg]) - rb[s], ra[s]);
+                        // ryg of this solve: w - G x at the x before the update (x = 0 at k = 0)
+                        const double ryg = d != 0.0 ? wv.w[s][lane] - (k == 0 ? 0.0 : dot4(c, xvv[sg])) : 0.0;
+                        ra[s] = fma(d, dot4(c, dy[sg]) - ryg, k == 0 ? 0.0 : ra[s]);
                     }
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg) {
@@ -782,16 +842,17 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
                             const int i = 2 * t + c;
-                            const double dbu = (boxed && su[sg][c] < zu[sg][c]) ? idl : 0.0;
-                            const double dbl = (boxed && sl[sg][c] < zl[sg][c]) ? idl : 0.0;
-                            const double ryu = dbu != 0.0 ? sh.ub[i] - vx[sg][c] : 0.0;
-                            const double ryl = dbl != 0.0 ? -sh.lb[i] + vx[sg][c] : 0.0;
-                            e1[sg][c] = fma(dbu, dv[sg][c] - ryu, e1[sg][c]);
-                            e2[sg][c] = fma(dbl, -dv[sg][c] - ryl, e2[sg][c]);
-                            vx[sg][c] = own[sg] ? vx[sg][c] + dv[sg][c] : 0.0;
+                            const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
+                            const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
+                            const double x_old = k == 0 ? 0.0 : BX(F_VX, sg, c);
+                            const double ryu = dbu != 0.0 ? sh.ub[i] - x_old : 0.0;
+                            const double ryl = dbl != 0.0 ? -sh.lb[i] + x_old : 0.0;
+                            BX(F_E1, sg, c) = fma(dbu, dv[sg][c] - ryu, k == 0 ? 0.0 : BX(F_E1, sg, c));
+                            BX(F_E2, sg, c) = fma(dbl, -dv[sg][c] - ryl, k == 0 ? 0.0 : BX(F_E2, sg, c));
+                            BX(F_VX, sg, c) = own[sg] ? x_old + dv[sg][c] : 0.0;
                         }
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) xvv[sg][a] += dy[sg][a];
+                        for (int a = 0; a < 4; ++a) xvv[sg][a] = (k == 0 ? 0.0 : xvv[sg][a]) + dy[sg][a];
                     }
                     if (k < POLISH_REFINE) {
                         // next right-hand side of the refinement
@@ -807,8 +868,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             cf(s, c);
                             const double d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
                             const double gx = dot4(c, xvv[sg]);
-                            rb[s] = d != 0.0 ? wv.w[s][lane] - gx : 0.0;
-                            const double t = -(ra[s] - d * rb[s]);
+                            const double ryg = d != 0.0 ? wv.w[s][lane] - gx : 0.0;
+                            const double t = -(ra[s] - d * ryg);
 #pragma unroll
                             for (int a = 0; a < 4; ++a) acc[sg][a] = fma(t, c[a], acc[sg][a]);
                         }
@@ -821,12 +882,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                             for (int c = 0; c < 2; ++c) {
                                 const int i = 2 * t + c;
-                                const double dbu = (boxed && su[sg][c] < zu[sg][c]) ? idl : 0.0;
-                                const double dbl = (boxed && sl[sg][c] < zl[sg][c]) ? idl : 0.0;
-                                const double ryu = dbu != 0.0 ? sh.ub[i] - vx[sg][c] : 0.0;
-                                const double ryl = dbl != 0.0 ? -sh.lb[i] + vx[sg][c] : 0.0;
-                                const double rx = fma(MT.R[c * 2], vx[sg][0], MT.R[c * 2 + 1] * vx[sg][1]);
-                                bu[c] = -q_[sg][c] - rx - e1[sg][c] + e2[sg][c] + dbu * ryu - dbl * ryl;
+                                const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
+                                const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
+                                const double ryu = dbu != 0.0 ? sh.ub[i] - BX(F_VX, sg, c) : 0.0;
+                                const double ryl = dbl != 0.0 ? -sh.lb[i] + BX(F_VX, sg, c) : 0.0;
+                                const double rx = M.Rmul(c, BX(F_VX, sg, 0), BX(F_VX, sg, 1));
+                                bu[c] = -BX(F_Q, sg, c) - rx - BX(F_E1, sg, c) + BX(F_E2, sg, c) + dbu * ryu - dbl * ryl;
                             }
                             if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
                         }
@@ -841,12 +902,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                                 const int i = 2 * (kseg[sg] - 1) + c;
                                 if (own[sg]) {
                                     if (boxed) {
-                                        viol = fmax(viol, fmax(vx[sg][c] - sh.ub[i], sh.lb[i] - vx[sg][c]));
+                                        viol = fmax(viol, fmax(BX(F_VX, sg, c) - sh.ub[i], sh.lb[i] - BX(F_VX, sg, c)));
                                         wsc = fmax(wsc, fmax(fabs(sh.lb[i]), fabs(sh.ub[i])));
                                     }
-                                    ysc = fmax(ysc, fmax(fabs(e1[sg][c]), fabs(e2[sg][c])));
-                                    ymin = fmin(ymin, fmin(e1[sg][c], e2[sg][c]));
-                                    fin = fin && isfinite(vx[sg][c]);
+                                    ysc = fmax(ysc, fmax(fabs(BX(F_E1, sg, c)), fabs(BX(F_E2, sg, c))));
+                                    ymin = fmin(ymin, fmin(BX(F_E1, sg, c), BX(F_E2, sg, c)));
+                                    fin = fin && isfinite(BX(F_VX, sg, c));
                                 }
                             }
                         bool paired[RS];
@@ -855,13 +916,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         if (P.r_partner) {
 #pragma unroll
                             for (int s = 0; s < RS; ++s)
-                                wv.scr[s][lane] = (rv[s] && s_[s] < z_[s]) ? ra[s] : NAN;
+                                scr[s][lane] = (rv[s] && s_[s] < z_[s]) ? ra[s] : NAN;
                             wb();
 #pragma unroll
                             for (int s = 0; s < RS; ++s) {
                                 const int pr = rv[s] ? sh.partner[s * G16 + j] : -1;
                                 paired[s] = pr >= 0 && s_[s] < z_[s] &&
-                                            !isnan(wv.scr[pr / G16][(lane & 48) + (pr % G16)]);
+                                            !isnan(scr[pr / G16][(lane & 48) + (pr % G16)]);
                             }
                             wb();
                         }
@@ -884,18 +945,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         ymin = row_min(ymin);
                         const double finv = row_min(fin ? 1.0 : 0.0);
                         if (finv > 0.0 && viol <= POLISH_TOL * (1.0 + wsc) && ymin >= -POLISH_TOL * (1.0 + ysc)) {
-                            status = CARMPC_OPTIMAL;
 #pragma unroll
                             for (int sg = 0; sg < 2; ++sg)
                                 if (own[sg]) {
-                                    const int t = kseg[sg] - 1;
-                                    u_out[inst * ld_u + 2 * t] = vx[sg][0];
-                                    u_out[inst * ld_u + 2 * t + 1] = vx[sg][1];
+                                    BX(F_U, sg, 0) = BX(F_VX, sg, 0);
+                                    BX(F_U, sg, 1) = BX(F_VX, sg, 1);
                                 }
-                            if (j == 0) {
-                                status_out[inst] = status;
-                                if (iters_out) iters_out[inst] = it;
-                            }
+                            finish(CARMPC_OPTIMAL, false);
                             active = false;
                         }
                         polish_failed = true;
@@ -903,21 +959,21 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     continue;
                 }
                 // ---------------- normal trip ----------------
+                // slot directions are rebuilt from the stage states of each solve (nothing per
+                // slot survives a pass): ds = -rp - c.dy, dz = (-rc - z ds)/s with rc = s z for the
+                // predictor and rc = s z + dsA dzA - smu for the corrector (dsA, dzA from dyA).
                 if (k == 0) {
-                    // predictor direction: ratio test, sigma, corrector right-hand side
                     double amax = INFINITY, mua = 0.0;
+                    double kd[2][2][4], dsv[RS], dzv[RS];
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
                         double c[4];
                         cf(s, c);
-                        const double w = wv.w[s][lane];
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - w : 0.0;
-                        const double ds = rv[s] ? -rp - dot4(c, dy[sg]) : 0.0;
-                        const double dz = rv[s] ? (-s_[s] * z_[s] - z_[s] * ds) * frcp(s_[s]) : 0.0;
-                        ra[s] = ds;
-                        rb[s] = dz;
-                        amax = fmin(amax, fmin(ratio(s_[s], ds), ratio(z_[s], dz)));
+                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
+                        dsv[s] = rv[s] ? -rp - dot4(c, dy[sg]) : 0.0;
+                        dzv[s] = rv[s] ? (-s_[s] * z_[s] - z_[s] * dsv[s]) * frcp(s_[s]) : 0.0;
+                        amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
                     }
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
@@ -925,31 +981,32 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         for (int c = 0; c < 2; ++c) {
                             const int i = 2 * (kseg[sg] - 1) + c;
                             if (own[sg] && boxed) {
-                                const double rpu = u_[sg][c] + su[sg][c] - sh.ub[i];
-                                const double rpl = -u_[sg][c] + sl[sg][c] + sh.lb[i];
+                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
+                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
+                                const double rpu = uu + su - sh.ub[i];
+                                const double rpl = -uu + sl + sh.lb[i];
                                 const double dsu = -rpu - dv[sg][c], dsl = -rpl + dv[sg][c];
-                                const double dzu = (-su[sg][c] * zu[sg][c] - zu[sg][c] * dsu) * frcp(su[sg][c]);
-                                const double dzl = (-sl[sg][c] * zl[sg][c] - zl[sg][c] * dsl) * frcp(sl[sg][c]);
-                                amax = fmin(amax, fmin(fmin(ratio(su[sg][c], dsu), ratio(zu[sg][c], dzu)),
-                                                       fmin(ratio(sl[sg][c], dsl), ratio(zl[sg][c], dzl))));
-                                pua[sg][c] = dsu * dzu;
-                                pla[sg][c] = dsl * dzl;
-                                e1[sg][c] = dsu;
-                                e2[sg][c] = dzu;
-                                e3[sg][c] = dsl;
-                                e4[sg][c] = dzl;
+                                const double dzu = (-su * zu - zu * dsu) * frcp(su);
+                                const double dzl = (-sl * zl - zl * dsl) * frcp(sl);
+                                amax = fmin(amax, fmin(fmin(ratio(su, dsu), ratio(zu, dzu)), fmin(ratio(sl, dsl), ratio(zl, dzl))));
+                                kd[sg][c][0] = dsu;
+                                kd[sg][c][1] = dzu;
+                                kd[sg][c][2] = dsl;
+                                kd[sg][c][3] = dzl;
                             }
                         }
                     const double a = fmin(1.0, row_min(amax));
 #pragma unroll
-                    for (int s = 0; s < RS; ++s) mua = fma(fma(a, ra[s], s_[s]), fma(a, rb[s], z_[s]), mua);
+                    for (int s = 0; s < RS; ++s) mua = fma(fma(a, dsv[s], s_[s]), fma(a, dzv[s], z_[s]), mua);
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                         for (int c = 0; c < 2; ++c)
                             if (own[sg] && boxed) {
-                                mua = fma(fma(a, e1[sg][c], su[sg][c]), fma(a, e2[sg][c], zu[sg][c]), mua);
-                                mua = fma(fma(a, e3[sg][c], sl[sg][c]), fma(a, e4[sg][c], zl[sg][c]), mua);
+                                mua = fma(fma(a, kd[sg][c][0], BX(F_SU, sg, c)), fma(a, kd[sg][c][1], BX(F_ZU, sg, c)), mua);
+                                mua = fma(fma(a, kd[sg][c][2], BX(F_SL, sg, c)), fma(a, kd[sg][c][3], BX(F_ZL, sg, c)), mua);
+                                BX(F_E1, sg, c) = kd[sg][c][0] * kd[sg][c][1];   // predictor products, kept for k = 1
+                                BX(F_E2, sg, c) = kd[sg][c][2] * kd[sg][c][3];
                             }
                     const double sg3 = row_sum(mua) * inv_m / mu;
                     smu = sg3 * sg3 * sg3 * mu;
@@ -963,14 +1020,16 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         const int sg = s / RSEG;
                         double c[4];
                         cf(s, c);
-                        const double pa = ra[s] * rb[s];
-                        ra[s] = pa;   // keep the predictor products for the corrector
                         const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
-                        const double rc = s_[s] * z_[s] + pa - smu;
+                        const double rc = s_[s] * z_[s] + dsv[s] * dzv[s] - smu;
                         const double t = rv[s] ? (rc - z_[s] * rp) * frcp(s_[s]) : 0.0;
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(t, c[aa], acc[sg][aa]);
                     }
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                        for (int aa = 0; aa < 4; ++aa) dyA[sg][aa] = dy[sg][aa];
                     double zero4[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
                     wb();
                     write_bx(acc, zero4, 0.0);
@@ -982,14 +1041,15 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         for (int c = 0; c < 2; ++c) {
                             const int i = 2 * t + c;
                             if (boxed) {
-                                const double rpu = u_[sg][c] + su[sg][c] - sh.ub[i];
-                                const double rpl = -u_[sg][c] + sl[sg][c] + sh.lb[i];
-                                const double rcu = su[sg][c] * zu[sg][c] + pua[sg][c] - smu;
-                                const double rcl = sl[sg][c] * zl[sg][c] + pla[sg][c] - smu;
-                                bu[c] = -rd_[sg][c] + (rcu - zu[sg][c] * rpu) * frcp(su[sg][c]) -
-                                        (rcl - zl[sg][c] * rpl) * frcp(sl[sg][c]);
+                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
+                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
+                                const double rpu = uu + su - sh.ub[i];
+                                const double rpl = -uu + sl + sh.lb[i];
+                                const double rcu = su * zu + BX(F_E1, sg, c) - smu;
+                                const double rcl = sl * zl + BX(F_E2, sg, c) - smu;
+                                bu[c] = -BX(F_RD, sg, c) + (rcu - zu * rpu) * frcp(su) - (rcl - zl * rpl) * frcp(sl);
                             } else {
-                                bu[c] = -rd_[sg][c];
+                                bu[c] = -BX(F_RD, sg, c);
                             }
                         }
                         if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
@@ -1007,11 +1067,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         double c[4];
                         cf(s, c);
                         const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
-                        const double rc = s_[s] * z_[s] + ra[s] - smu;
-                        const double ds = rv[s] ? -rp - dot4(c, dy[sg]) : 0.0;
+                        const double dsa = -rp - dot4(c, dyA[sg]);
+                        const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
+                        const double rc = s_[s] * z_[s] + dsa * dza - smu;
+                        const double ds = -rp - dot4(c, dy[sg]);
                         const double dz = rv[s] ? (-rc - z_[s] * ds) * frcp(s_[s]) : 0.0;
-                        ra[s] = ds;
-                        rb[s] = dz;
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(-dz, c[aa], acc[sg][aa]);
                     }
@@ -1026,75 +1086,90 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             const int i = 2 * t + c;
                             double dzu = 0.0, dzl = 0.0;
                             if (own[sg] && boxed) {
-                                const double rpu = u_[sg][c] + su[sg][c] - sh.ub[i];
-                                const double rpl = -u_[sg][c] + sl[sg][c] + sh.lb[i];
-                                const double rcu = su[sg][c] * zu[sg][c] + pua[sg][c] - smu;
-                                const double rcl = sl[sg][c] * zl[sg][c] + pla[sg][c] - smu;
+                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
+                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
+                                const double rpu = uu + su - sh.ub[i];
+                                const double rpl = -uu + sl + sh.lb[i];
+                                const double rcu = su * zu + BX(F_E1, sg, c) - smu;
+                                const double rcl = sl * zl + BX(F_E2, sg, c) - smu;
                                 const double dsu = -rpu - dv[sg][c], dsl = -rpl + dv[sg][c];
-                                dzu = (-rcu - zu[sg][c] * dsu) * frcp(su[sg][c]);
-                                dzl = (-rcl - zl[sg][c] * dsl) * frcp(sl[sg][c]);
-                                e1[sg][c] = dsu;
-                                e2[sg][c] = dzu;
-                                e3[sg][c] = dsl;
-                                e4[sg][c] = dzl;
+                                dzu = (-rcu - zu * dsu) * frcp(su);
+                                dzl = (-rcl - zl * dsl) * frcp(sl);
+                                BX(F_E1, sg, c) = dsu;
+                                BX(F_E2, sg, c) = dzu;
+                                BX(F_E3, sg, c) = dsl;
+                                BX(F_E4, sg, c) = dzl;
                             }
-                            const double rdu = fma(MT.R[c * 2], dv[sg][0], MT.R[c * 2 + 1] * dv[sg][1]);
-                            bu[c] = -(rdu + rd_[sg][c] + (dzu - dzl));
+                            const double rdu = M.Rmul(c, dv[sg][0], dv[sg][1]);
+                            bu[c] = -(rdu + BX(F_RD, sg, c) + (dzu - dzl));
                         }
 #pragma unroll
-                        for (int c = 0; c < 2; ++c) vx[sg][c] = dv[sg][c];
+                        for (int c = 0; c < 2; ++c) BX(F_VX, sg, c) = dv[sg][c];
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) xvv[sg][aa] = dy[sg][aa];
                         if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
                     }
                 } else if (k == 2) {
-                    // apply the correction, step length, update
-                    double amax = INFINITY;
+                    // corrected direction (dy_T = corrector + correction), step length, update
+                    double dyT[2][4];
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                        for (int aa = 0; aa < 4; ++aa) dyT[sg][aa] = xvv[sg][aa] + dy[sg][aa];
+                    double amax = INFINITY, dsv[RS], dzv[RS];
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
                         double c[4];
                         cf(s, c);
-                        const double cs = rv[s] ? -dot4(c, dy[sg]) : 0.0;
-                        ra[s] += cs;
-                        rb[s] = rv[s] ? rb[s] - z_[s] * cs * frcp(s_[s]) : 0.0;
-                        amax = fmin(amax, fmin(ratio(s_[s], ra[s]), ratio(z_[s], rb[s])));
+                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
+                        const double dsa = -rp - dot4(c, dyA[sg]);
+                        const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
+                        const double rc = s_[s] * z_[s] + dsa * dza - smu;
+                        dsv[s] = rv[s] ? -rp - dot4(c, dyT[sg]) : 0.0;
+                        dzv[s] = rv[s] ? (-rc - z_[s] * dsv[s]) * frcp(s_[s]) : 0.0;
+                        amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
                     }
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
-                            vx[sg][c] += dv[sg][c];
+                            BX(F_VX, sg, c) += dv[sg][c];
                             if (own[sg] && boxed) {
                                 const double cu = dv[sg][c];
-                                e1[sg][c] -= cu;
-                                e2[sg][c] = fma(zu[sg][c] * cu, frcp(su[sg][c]), e2[sg][c]);
-                                e3[sg][c] += cu;
-                                e4[sg][c] = fma(-zl[sg][c] * cu, frcp(sl[sg][c]), e4[sg][c]);
-                                amax = fmin(amax, fmin(fmin(ratio(su[sg][c], e1[sg][c]), ratio(zu[sg][c], e2[sg][c])),
-                                                       fmin(ratio(sl[sg][c], e3[sg][c]), ratio(zl[sg][c], e4[sg][c]))));
+                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
+                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c);
+                                const double e1 = BX(F_E1, sg, c) - cu;
+                                const double e2 = fma(zu * cu, frcp(su), BX(F_E2, sg, c));
+                                const double e3 = BX(F_E3, sg, c) + cu;
+                                const double e4 = fma(-zl * cu, frcp(sl), BX(F_E4, sg, c));
+                                BX(F_E1, sg, c) = e1;
+                                BX(F_E2, sg, c) = e2;
+                                BX(F_E3, sg, c) = e3;
+                                BX(F_E4, sg, c) = e4;
+                                amax = fmin(amax, fmin(fmin(ratio(su, e1), ratio(zu, e2)), fmin(ratio(sl, e3), ratio(zl, e4))));
                             }
                         }
                     const double a = fmin(1.0, STEP_FRAC * row_min(amax));
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
-                        s_[s] = fma(a, ra[s], s_[s]);
-                        z_[s] = fma(a, rb[s], z_[s]);
+                        s_[s] = fma(a, dsv[s], s_[s]);
+                        z_[s] = fma(a, dzv[s], z_[s]);
                     }
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg) {
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
-                            if (own[sg]) u_[sg][c] = fma(a, vx[sg][c], u_[sg][c]);
+                            if (own[sg]) BX(F_U, sg, c) = fma(a, BX(F_VX, sg, c), BX(F_U, sg, c));
                             if (own[sg] && boxed) {
-                                su[sg][c] = fma(a, e1[sg][c], su[sg][c]);
-                                zu[sg][c] = fma(a, e2[sg][c], zu[sg][c]);
-                                sl[sg][c] = fma(a, e3[sg][c], sl[sg][c]);
-                                zl[sg][c] = fma(a, e4[sg][c], zl[sg][c]);
+                                BX(F_SU, sg, c) = fma(a, BX(F_E1, sg, c), BX(F_SU, sg, c));
+                                BX(F_ZU, sg, c) = fma(a, BX(F_E2, sg, c), BX(F_ZU, sg, c));
+                                BX(F_SL, sg, c) = fma(a, BX(F_E3, sg, c), BX(F_SL, sg, c));
+                                BX(F_ZL, sg, c) = fma(a, BX(F_E4, sg, c), BX(F_ZL, sg, c));
                             }
                         }
 #pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) xs[sg][aa] = fma(a, xvv[sg][aa] + dy[sg][aa], xs[sg][aa]);
+                        for (int aa = 0; aa < 4; ++aa) xs[sg][aa] = fma(a, dyT[sg][aa], xs[sg][aa]);
                     }
                     polish_failed = false;
                     ++it;
@@ -1136,9 +1211,10 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
                            status, iters, s);
         return hipGetLastError();
     };
+    const bool bike = P.ric == 2;
     switch (P.N) {
-        case 10: return go(ipm_riccati_kernel<10, WPB>);
-        case 20: return go(ipm_riccati_kernel<20, WPB>);
+        case 10: return bike ? go(ipm_riccati_kernel<10, WPB, BicycleModel>) : go(ipm_riccati_kernel<10, WPB, DenseModel>);
+        case 20: return bike ? go(ipm_riccati_kernel<20, WPB, BicycleModel>) : go(ipm_riccati_kernel<20, WPB, DenseModel>);
         default: *unsupported = 1; return hipErrorInvalidValue;
     }
 }
