@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=PER_GPU)
     ap.add_argument("--cpu-sample", type=int, default=24576)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 3 dense 1-wave/SIMD)")
+    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 3 dense 1-wave/SIMD, 7 riccati)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -172,13 +172,16 @@ def main():
     value = total / wall_max
     status_split = {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
                                                                       "numerical"))}
-    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 4: "ipm_staged_readlane", 5: "ipm_staged_4wave", 6: "ipm_staged_ldl"}
+    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 4: "ipm_staged_readlane", 5: "ipm_staged_4wave", 6: "ipm_staged_ldl",
+             7: "ipm_riccati"}
     kdesc = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
              2: "ipm_staged (wavefront per QP, stage-structured G/H products and Riccati-style M build)",
              3: "ipm_dense, 4 waves per workgroup",
              4: "ipm_staged with the readlane-broadcast Cholesky (A/B variant)",
              5: "ipm_staged, 4 waves per workgroup (512 registers per wave)",
-             6: "ipm_staged with the square-root-free LDL' (A/B variant)"}
+             6: "ipm_staged with the square-root-free LDL' (A/B variant)",
+             7: "ipm_riccati (16 lanes per QP, 4 QPs per wavefront, row state in registers, stage-form Riccati "
+                "factorization and solves, per-group instance refill)"}
     used = sorted(set(kernels))
     out = {
         "metric": "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X",

@@ -337,7 +337,8 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
 hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, const double* xref, double* u_out,
                         int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
-    if (s.kernel == 7) return launch_riccati(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (s.kernel == 7 || (s.kernel == 0 && D.ric))
+        return launch_riccati(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     const bool staged = (s.kernel >= 4 && s.kernel <= 6) || s.kernel == 2 || (s.kernel == 0 && D.staged);
     if (staged) return launch_staged(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     return launch_dense(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
@@ -351,7 +352,7 @@ const char* carmpc_version(void) { return "carmpc-mi355x 0.2 (gfx950, dense + st
 
 int carmpc_problem_kernel(const carmpc_problem* P) {
     if (!P) return fail(CARMPC_EINVAL, "null problem");
-    return P->dev.staged ? 2 : 1;
+    return P->dev.ric ? 7 : (P->dev.staged ? 2 : 1);
 }
 
 // Flops one IPM iteration (predictor + corrector + one refinement) of the given kernel
@@ -359,6 +360,15 @@ int carmpc_problem_kernel(const carmpc_problem* P) {
 double carmpc_executed_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
     if (!P) return 0.0;
     const double n = P->dev.n, p = P->dev.p, N = P->dev.N;
+    if (kernel == 7 || (kernel == 0 && P->dev.ric)) {
+        // grouped Riccati kernel, one copy of the (16-lane redundant) stage recursions:
+        // per stage factorization + adjoint + 2 backward + 3 forward passes, per row the five
+        // row phases (~212 flops), per input the box rows; bicycle sparsity when selected
+        const bool bike = P->dev.ric == 2;
+        const double fac = bike ? 250.0 : 470.0, adj = bike ? 44.0 : 104.0, back = bike ? 42.0 : 72.0,
+                     fwd = bike ? 34.0 : 64.0;
+        return N * (fac + adj + 2.0 * back + 3.0 * fwd) + 212.0 * p + 60.0 * n;
+    }
     const bool staged = (kernel >= 4 && kernel <= 6) || kernel == 2 || (kernel == 0 && P->dev.staged);
     const double chol = n * n * n / 3.0, trisolve = 2.0 * n * n;
     if (!staged) {

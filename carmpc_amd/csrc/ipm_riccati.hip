@@ -24,6 +24,32 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+// Optional per-phase cycle accounting (profiling build only: -DCARMPC_PHASE_TIMING,
+// tools/ric_timing.py): 0 init, 1 residual rows, 2 adjoint pass, 3 decisions, 4 factor rows,
+// 5 factorization pass, 6 backward passes, 7 forward passes, 8-10 row phases k = 0..2,
+// 11 polish rows.
+#ifdef CARMPC_PHASE_TIMING
+__device__ unsigned long long carmpc_ric_cycles[12];
+#define RT_DECL                                                        \
+    unsigned long long rt_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+    unsigned long long rt_t = clock64();
+#define RT_MARK(i)                               \
+    do {                                         \
+        const unsigned long long n_ = clock64(); \
+        rt_acc[i] += n_ - rt_t;                  \
+        rt_t = n_;                               \
+    } while (0)
+#define RT_FLUSH()                                                                           \
+    do {                                                                                     \
+        if (lane == 0)                                                                       \
+            for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&carmpc_ric_cycles[i_], rt_acc[i_]); \
+    } while (0)
+#else
+#define RT_DECL
+#define RT_MARK(i) do {} while (0)
+#define RT_FLUSH() do {} while (0)
+#endif
+
 namespace carmpc {
 
 namespace {
@@ -229,41 +255,50 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         wb();
         double pv[4];
         rd4((N - 1) * REC + O_BX, pv);
+        // stage data one stage ahead (software pipelining of the LDS latency)
+        auto ld = [&](int t, double (&bu)[2], double (&ch)[4], double (&K)[8], double (&bx)[4]) {
+            const int r = t * REC;
+            rd2(r + O_BU, bu[0], bu[1]);
+            rd2(r + O_CH, ch[0], ch[1]);
+            rd2(r + O_CH + 2, ch[2], ch[3]);
+            rdK(r, K);
+            rd4((t >= 1 ? r - REC : 0) + O_BX, bx);
+        };
+        double bu[2], ch[4], K[8], bx[4];
+        ld(N - 1, bu, ch, K, bx);
 #pragma unroll 1
         for (int t = N - 1; t >= 0; --t) {
-            const int r = t * REC;
-            double bu0, bu1, il00, l10, il11, dummy;
-            rd2(r + O_BU, bu0, bu1);
-            rd2(r + O_CH, il00, l10);
-            rd2(r + O_CH + 2, il11, dummy);
-            double K[8];
-            rdK(r, K);
-            double g0 = bu0, g1 = bu1;
+            double nbu[2], nch[4], nK[8], nbx[4];
+            ld(t >= 1 ? t - 1 : 0, nbu, nch, nK, nbx);
+            double g0 = bu[0], g1 = bu[1];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 g0 = M.B_(a, 0, pv[a], g0);
                 g1 = M.B_(a, 1, pv[a], g1);
             }
+            const double il00 = ch[0], l10 = ch[1], il11 = ch[2];
             const double y0 = g0 * il00;
             const double y1 = fma(-l10, y0, g1) * il11;
             const double k1 = y1 * il11;
             const double k0 = fma(-l10, k1, y0) * il00;
-            if (j == 0) wr2(r + O_DB, k0, k1);
-            if (t >= 1) {
-                double bx[4];
-                rd4(r - REC + O_BX, bx);
-                double np[4];
+            if (j == 0) wr2(t * REC + O_DB, k0, k1);
+            double np[4];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    double acc = bx[a];
+            for (int a = 0; a < 4; ++a) {
+                double acc = bx[a];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
-                    acc = fma(-K[a], g0, acc);
-                    np[a] = fma(-K[4 + a], g1, acc);
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a) pv[a] = np[a];
+                for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
+                acc = fma(-K[a], g0, acc);
+                np[a] = fma(-K[4 + a], g1, acc);
             }
+#pragma unroll
+            for (int a = 0; a < 4; ++a) pv[a] = np[a];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) K[e] = nK[e];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { ch[e] = nch[e]; bx[e] = nbx[e]; }
+            bu[0] = nbu[0];
+            bu[1] = nbu[1];
         }
         wb();
     };
@@ -271,14 +306,17 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto forward = [&]() {
         wb();
         double y[4] = {0.0, 0.0, 0.0, 0.0};
+        double K[8], kp[2];
+        rdK(0, K);
+        rd2(O_DB, kp[0], kp[1]);
 #pragma unroll 1
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
-            double k0, k1;
-            rd2(r + O_DB, k0, k1);
-            double K[8];
-            rdK(r, K);
-            double v0 = k0, v1 = k1;
+            const int rn = (t + 1 < N ? t + 1 : t) * REC;
+            double nK[8], nkp[2];
+            rdK(rn, nK);
+            rd2(rn + O_DB, nkp[0], nkp[1]);
+            double v0 = kp[0], v1 = kp[1];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 v0 = fma(-K[a], y[a], v0);
@@ -299,6 +337,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 wr4(r + O_BX, y);
                 wr2(r + O_BU, v0, v1);
             }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) K[e] = nK[e];
+            kp[0] = nkp[0];
+            kp[1] = nkp[1];
         }
         wb();
     };
@@ -342,12 +384,23 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 for (int b = a; b < 4; ++b) Pm[sym10(a, b)] = MT.P[a * 4 + b] + Wn[sym10(a, b)];
             rd4((N - 1) * REC + O_BX, pv);
         }
+        // stage data one stage ahead: Db_t, b^u_t (record t), W_t, b^x_t (record t-1)
+        auto ld = [&](int t, double (&du)[4], double (&Wt)[10], double (&bx)[4]) {
+            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
+            rd2(r + O_DB, du[0], du[1]);
+            rd2(r + O_BU, du[2], du[3]);
+#pragma unroll
+            for (int e = 0; e < 5; ++e) rd2(rp + 2 * e, Wt[2 * e], Wt[2 * e + 1]);
+            rd4(rp + O_BX, bx);
+        };
+        double du[4], Wt[10], bx[4];
+        ld(N - 1, du, Wt, bx);
 #pragma unroll 1
         for (int t = N - 1; t >= 0; --t) {
             const int r = t * REC;
-            double db0, db1, bu0, bu1;
-            rd2(r + O_DB, db0, db1);
-            rd2(r + O_BU, bu0, bu1);
+            double ndu[4], nWt[10], nbx[4];
+            ld(t >= 1 ? t - 1 : 0, ndu, nWt, nbx);
+            const double db0 = du[0], db1 = du[1], bu0 = du[2], bu1 = du[3];
             // PB = P B (4x2); Re = R + diag(Db) + B'PB; F = B'PA = (PB)'A
             double PB[4][2];
 #pragma unroll
@@ -411,10 +464,6 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 wr2(r + O_DB, k0, k1);
             }
             if (t >= 1) {
-                double Wt[10], bx[4];
-#pragma unroll
-                for (int e = 0; e < 5; ++e) rd2(r - REC + 2 * e, Wt[2 * e], Wt[2 * e + 1]);
-                rd4(r - REC + O_BX, bx);
                 // P_t = Qbar_t + W_t + A'PA - F'K  (upper triangle), PA one column at a time
                 double Pn[10];
 #pragma unroll
@@ -450,6 +499,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                 for (int a = 0; a < 4; ++a) pv[a] = np[a];
             }
+#pragma unroll
+            for (int e = 0; e < 10; ++e) Wt[e] = nWt[e];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { du[e] = ndu[e]; bx[e] = nbx[e]; }
         }
         wb();
     };
@@ -483,8 +536,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         live = inst < batch;
         fresh = true;
     };
+    RT_DECL
     while (__any(live)) {
         bool active = live;
+        RT_MARK(11);
         if (live && fresh) {
             fresh = false;
             double xv0[NX], xr[NX];
@@ -571,6 +626,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 qnorm = 1.0 + row_max(qn);
             }
         }
+        RT_MARK(0);
         if (!__any(active)) continue;
         {
             // ================= residuals (R1 + B1) =================
@@ -627,6 +683,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         wr4((kseg[sg] - 1) * REC + 0, v);
                         wr4((kseg[sg] - 1) * REC + 4, h);
                     }
+                RT_MARK(1);
                 mu = row_sum(musum) * inv_m;
                 rpn = row_max(rpn);
                 gun = row_max(gun);
@@ -637,12 +694,15 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 wb();
                 {
                     double pz[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};
+                    double lzv[4], lhv[4];
+                    rd4((N - 1) * REC + 0, lzv);
+                    rd4((N - 1) * REC + 4, lhv);
 #pragma unroll 1
                     for (int t = N - 1; t >= 0; --t) {
                         const int r = t * REC;
-                        double lzv[4], lhv[4];
-                        rd4(r + 0, lzv);
-                        rd4(r + 4, lhv);
+                        double nlz[4], nlh[4];
+                        rd4((t >= 1 ? r - REC : 0), nlz);
+                        rd4((t >= 1 ? r - REC : 0) + 4, nlh);
                         double nz[4], nh[4];
 #pragma unroll
                         for (int a = 0; a < 4; ++a) {
@@ -672,14 +732,16 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             lo += fmin(az * lb, az * ub);
                             scf = fma(fabs(az), fmax(fabs(lb), fabs(ub)), scf);
                         }
-                        wb();
                         if (j == 0) {
                             wr2(r + 12, gz[0], gz[1]);
                             wr2(r + 14, hs[0], hs[1]);
                         }
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) { lzv[a] = nlz[a]; lhv[a] = nlh[a]; }
                     }
                 }
                 wb();
+                RT_MARK(2);
                 double rdn = 0.0, hun = 0.0, gzn = 0.0;
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg) {
@@ -726,6 +788,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 }
             }
             const bool any_polish = __any(polish);
+            RT_MARK(3);
             if (!__any(active)) continue;
             // ================= factorization rows (R2) + first right-hand side =================
             // normal: d = z/s, predictor rhs; polish: d = 1/delta on the active set (s < z)
@@ -806,7 +869,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         wr2(r + O_DB, db[0], db[1]);
                     }
                 }
+                RT_MARK(4);
                 factor_and_back();
+                RT_MARK(5);
             }
             // ================= solves =================
             // fully unrolled: k is a constant in every branch below (precise register lifetimes)
@@ -815,7 +880,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 if (k == 3 && !any_polish) break;
                 const bool run = active && (polish || k < 3);
                 if (k > 0 && run) back_linear();
+                RT_MARK(6);
                 if (run) forward();
+                RT_MARK(7);
                 if (!run) continue;
                 double dy[2][4], dv[2][2];
 #pragma unroll
@@ -956,6 +1023,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         }
                         polish_failed = true;
                     }
+                    RT_MARK(11);
                     continue;
                 }
                 // ---------------- normal trip ----------------
@@ -1054,6 +1122,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         }
                         if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
                     }
+                    RT_MARK(8);
                 } else if (k == 1) {
                     // corrector direction; refinement right-hand side -(H du + G'dz + rd + box)
                     double acc[2][4];
@@ -1109,6 +1178,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         for (int aa = 0; aa < 4; ++aa) xvv[sg][aa] = dy[sg][aa];
                         if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
                     }
+                    RT_MARK(9);
                 } else if (k == 2) {
                     // corrected direction (dy_T = corrector + correction), step length, update
                     double dyT[2][4];
@@ -1173,10 +1243,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     }
                     polish_failed = false;
                     ++it;
+                    RT_MARK(10);
                 }
             }
         }
     }
+    RT_FLUSH();
 }
 
 }  // namespace
@@ -1220,3 +1292,16 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
 }
 
 }  // namespace carmpc
+
+#ifdef CARMPC_PHASE_TIMING
+// Profiling build only: read (and optionally reset) the Riccati kernel's phase cycles.
+extern "C" int carmpc_debug_ric_cycles(unsigned long long* out12, int reset) {
+    if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(carmpc_ric_cycles), sizeof(unsigned long long) * 12) != hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned long long z[12] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(carmpc_ric_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

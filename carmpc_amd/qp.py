@@ -55,7 +55,8 @@ class SolverSettings:
     tol: float = 1e-10
     tol_mu: float = 1e-12
     max_iter: int = 60
-    #: 0 auto (staged when the problem has a stage layout), 1 dense, 2 staged, 3 dense 4-wave
+    #: 0 auto (grouped Riccati, else staged, else dense), 1 dense, 2 staged, 3 dense 4-wave,
+    #: 4-6 staged A/B variants, 7 grouped Riccati
     kernel: int = 0
 
     def c(self) -> Settings:
@@ -119,7 +120,7 @@ class QPProblem:
         vals = [ctypes.c_int32() for _ in range(5)]
         check(_native.load().carmpc_problem_info(self._h, *[ctypes.byref(v) for v in vals]), "carmpc_problem_info")
         self.n, self.p, self.npre, self.nx, _ = (v.value for v in vals)
-        #: solve kernel chosen by ``kernel=0`` (auto): 1 dense, 2 staged
+        #: solve kernel chosen by ``kernel=0`` (auto): 1 dense, 2 staged, 7 grouped Riccati
         self.kernel = int(_native.load().carmpc_problem_kernel(self._h))
 
     def __del__(self):

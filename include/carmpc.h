@@ -84,15 +84,18 @@ typedef struct {
     double tol;        /* primal/dual residual tolerance, relative to 1+||.||_inf */
     double tol_mu;     /* complementarity tolerance (absolute)                     */
     int32_t max_iter;
-    int32_t kernel;    /* 0 = auto (staged when the problem has one), 1 = dense (G,H in
-                          LDS), 2 = staged (stage structure, assembled problems with nu=2
-                          and a compiled N), 3 = dense with 4 waves per workgroup */
+    int32_t kernel;    /* 0 = auto (grouped Riccati, else staged, else dense), 1 = dense
+                          (G,H in LDS), 2 = staged (stage structure, assembled problems
+                          with nu=2 and a compiled N), 3 = dense with 4 waves per
+                          workgroup, 4-6 staged A/B variants, 7 = grouped stage-form
+                          (Riccati) kernel, 16 lanes per QP (assembled, nu=2, N in
+                          {10,20}, <= 8 rows per stage) */
 } carmpc_settings;
 
-/* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged. */
+/* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged, 7 grouped Riccati. */
 int carmpc_problem_kernel(const carmpc_problem* prob);
 
-/* Flops per IPM iteration the given kernel (0 auto, 1 dense, 2 staged) executes; the
+/* Flops per IPM iteration the given kernel (0 auto, 1 dense, 2 staged, 7 Riccati) executes; the
  * canonical dense count of SURVEY §8d is carmpc_canonical_flops_per_iter. */
 double carmpc_executed_flops_per_iter(const carmpc_problem* prob, int32_t kernel);
 

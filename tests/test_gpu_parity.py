@@ -58,7 +58,7 @@ def test_assembly_kernel_matches_oracle(gpu_available, name, N):
     np.testing.assert_allclose(m["S"], golden["S"], rtol=0, atol=1e-13)
 
 
-KERNELS = [1, 2, 4, 5, 6]   # carmpc_settings.kernel: dense; staged (default); staged A/B variants
+KERNELS = [1, 2, 4, 5, 6, 7]   # carmpc_settings.kernel: dense; staged; staged A/B variants; riccati (default)
 
 
 def _settings(kernel):
@@ -66,11 +66,11 @@ def _settings(kernel):
     return SolverSettings(kernel=kernel)
 
 
-def test_staged_layout_selected(gpu_available):
-    """Every reference configuration (N in {10, 20}, nu = 2) gets the staged kernel by default."""
+def test_riccati_layout_selected(gpu_available):
+    """Every reference configuration (N in {10, 20}, nu = 2) gets the grouped Riccati kernel by default."""
     for name, N in CONFIGS:
         _, qp = _setup(name, N)
-        assert qp.kernel == 2, (name, N)
+        assert qp.kernel == 7, (name, N)
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -180,7 +180,7 @@ def test_terminal_fallback_and_short_horizon(gpu_available, tmp_path):
         assert ((sc == 0) | (sc == 1)).all()   # equality pairs handled: no iteration-limit stops
         if N == 10:
             assert (sc == 0).all()
-        for kernel in [1] + ([2] if qp.kernel == 2 else []):
+        for kernel in [1] + ([2] if qp.kernel in (2, 7) else []) + ([7] if qp.kernel == 7 else []):
             u, st, _ = qp.solve(torch.as_tensor(X).cuda(), settings=_settings(kernel))
             st = st.cpu().numpy()
             np.testing.assert_array_equal(st, sc, err_msg=f"N={N} kernel {kernel}")
