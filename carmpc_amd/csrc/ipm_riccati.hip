@@ -130,10 +130,12 @@ struct Mt {
     __device__ __forceinline__ double R_(int c, int d, double x, double acc) const {
         return ((SP::R >> (c * 2 + d)) & 1u) ? fma(m.R[c * 2 + d], x, acc) : acc;
     }
-    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : 0.0; }
-    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : 0.0; }
+    // structural zeros are returned / accumulated as -0.0: x + (-0.0) == x and
+    // fma(a, b, -0.0) == a * b exactly, so the compiler drops them
+    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : -0.0; }
+    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : -0.0; }
     // (R v)_c
-    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, 0.0)); }
+    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, -0.0)); }
 };
 
 template <int N, int WPB, class SP>
@@ -220,10 +222,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto add_qbar = [&](bool termN, const double (&v)[4], double (&y)[4], double sgn) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            double accp = 0.0, accq = 0.0;
+            double accp = -0.0, accq = -0.0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                accp = fma(MT.P[a * 4 + b], v[b], accp);
+                accp = fma(MT.P[(a < b ? a : b) * 4 + (a < b ? b : a)], v[b], accp);
                 accq = M.Q_(a, b, v[b], accq);
             }
             y[a] = fma(sgn, termN ? accp : accq, y[a]);
@@ -325,7 +327,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double ny[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                double acc = M.B_(a, 0, v0, 0.0);
+                double acc = M.B_(a, 0, v0, -0.0);
                 acc = M.B_(a, 1, v1, acc);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
@@ -356,7 +358,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double ny[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                double acc = M.B_(a, 0, v0, 0.0);
+                double acc = M.B_(a, 0, v0, -0.0);
                 acc = M.B_(a, 1, v1, acc);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
@@ -407,7 +409,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             for (int a = 0; a < 4; ++a)
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    double acc = 0.0;
+                    double acc = -0.0;
 #pragma unroll
                     for (int b = 0; b < 4; ++b) acc = M.B_(b, c, Pm[sym10(a, b)], acc);
                     PB[a][c] = acc;
@@ -424,7 +426,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             for (int c = 0; c < 2; ++c)
 #pragma unroll
                 for (int mm = 0; mm < 4; ++mm) {
-                    double acc = 0.0;
+                    double acc = -0.0;
 #pragma unroll
                     for (int a = 0; a < 4; ++a) acc = M.A_(a, mm, PB[a][c], acc);
                     F[c][mm] = acc;
@@ -471,7 +473,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     double col[4];
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        double acc = 0.0;
+                        double acc = -0.0;
 #pragma unroll
                         for (int d = 0; d < 4; ++d) acc = M.A_(d, b, Pm[sym10(c, d)], acc);
                         col[c] = acc;
@@ -634,11 +636,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double lo = 0.0, scf = 0.0;
             bool polish = false;
             if (active) {
-                double lz[2][4], musum = 0.0;
+                double lz[2][4], musum = -0.0;
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) lz[sg][a] = 0.0;
+                    for (int a = 0; a < 4; ++a) lz[sg][a] = -0.0;
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
                     const int sg = s / RSEG;
@@ -676,7 +678,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg)
                     if (own[sg]) {
-                        double v[4], h[4] = {0.0, 0.0, 0.0, 0.0};
+                        double v[4], h[4] = {-0.0, -0.0, -0.0, -0.0};
 #pragma unroll
                         for (int a = 0; a < 4; ++a) v[a] = isN[sg] ? pn[a] : lz[sg][a];
                         add_qbar(kseg[sg] == N, xs[sg], h, 1.0);
@@ -718,7 +720,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         double gz[2], hs[2];
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
-                            double az = 0.0, ah = 0.0;
+                            double az = -0.0, ah = -0.0;
 #pragma unroll
                             for (int a = 0; a < 4; ++a) {
                                 pz[a] = nz[a];
@@ -801,9 +803,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg) {
 #pragma unroll
-                    for (int e = 0; e < 10; ++e) Wa[sg][e] = 0.0;
+                    for (int e = 0; e < 10; ++e) Wa[sg][e] = -0.0;
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) acc[sg][a] = 0.0;
+                    for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
                 }
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
@@ -927,7 +929,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                         for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-                            for (int a = 0; a < 4; ++a) acc[sg][a] = 0.0;
+                            for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
 #pragma unroll
                         for (int s = 0; s < RS; ++s) {
                             const int sg = s / RSEG;
@@ -1031,7 +1033,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 // slot survives a pass): ds = -rp - c.dy, dz = (-rc - z ds)/s with rc = s z for the
                 // predictor and rc = s z + dsA dzA - smu for the corrector (dsA, dzA from dyA).
                 if (k == 0) {
-                    double amax = INFINITY, mua = 0.0;
+                    double amax = INFINITY, mua = -0.0;
                     double kd[2][2][4], dsv[RS], dzv[RS];
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
@@ -1082,7 +1084,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = 0.0;
+                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
@@ -1129,7 +1131,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = 0.0;
+                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
