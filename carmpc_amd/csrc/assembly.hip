@@ -143,16 +143,20 @@ __global__ void pack_rows_kernel(PackArgs a) {
 
 // Luenberger observer (mpc.py:439-448): xhat <- A xhat + B uprev + L (y - C xhat)
 
+// With a.dhat (MPCOutputFBWithDisturbance, mpc.py:598-612): innovation e = y - C xhat - Cd d,
+// xhat <- A xhat + Bd d + B uprev + L e,  d <- d + L2 . e.
 __global__ void observer_kernel(ObsArgs a) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= a.batch) return;
     double x[NX], innov[8];
 #pragma unroll
     for (int k = 0; k < NX; ++k) x[k] = a.xhat[b * NX + k];
+    const double d = a.dhat ? a.dhat[b] : 0.0;
     for (int r = 0; r < a.ny; ++r) {
         double v = a.y[b * a.ny + r];
 #pragma unroll
         for (int k = 0; k < NX; ++k) v -= a.C[r * NX + k] * x[k];
+        if (a.dhat) v -= a.Cd[r] * d;
         innov[r] = v;
     }
     double out[NX];
@@ -161,12 +165,18 @@ __global__ void observer_kernel(ObsArgs a) {
         double v = 0.0;
 #pragma unroll
         for (int k = 0; k < NX; ++k) v += a.A[i * NX + k] * x[k];
+        if (a.dhat) v += a.Bd[i] * d;
         for (int c = 0; c < a.nu; ++c) v += a.B[i * a.nu + c] * a.uprev[b * a.ld_uprev + c];
         for (int r = 0; r < a.ny; ++r) v += a.L[i * a.ny + r] * innov[r];
         out[i] = v;
     }
 #pragma unroll
     for (int k = 0; k < NX; ++k) a.xhat[b * NX + k] = out[k];
+    if (a.dhat) {
+        double dn = d;
+        for (int r = 0; r < a.ny; ++r) dn += a.L2[r] * innov[r];
+        a.dhat[b] = dn;
+    }
 }
 
 // Nonlinear kinematic bicycle, forward Euler (simulator.py:51-69); input

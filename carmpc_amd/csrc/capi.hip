@@ -28,6 +28,13 @@ struct carmpc_problem {
     // assembled full matrices (device), for carmpc_problem_get
     double *T = nullptr, *S = nullptr, *H = nullptr, *h = nullptr, *G_all = nullptr, *E_all = nullptr,
            *w0_all = nullptr;
+    // host bookkeeping for the disturbance offsets (carmpc_problem_set_disturbance)
+    double A_host[16] = {};
+    const double* coef_all_dev = nullptr;   // p_all x NX row coefficients on x_k
+    const int32_t* stage_all_dev = nullptr; // p_all
+    std::vector<double> nrm_all;            // p_all condensed row norms
+    std::vector<int32_t> qp_rows, pre_rows; // packed QP rows / x0-only rows (assembled indices)
+    std::vector<int32_t> stage_slot, ric_slot;   // slot of each packed row per layout (empty: none)
     ~carmpc_problem() {
         for (void* p : allocs) (void)hipFree(p);
     }
@@ -69,7 +76,7 @@ hipError_t upload(carmpc_problem* P, T_** dst, const T_* src, size_t count) {
 }
 
 Settings make_settings(const carmpc_settings* s) {
-    Settings out{1e-10, 1e-12, 60, 0};
+    Settings out{1e-10, 1e-12, 60, 0, nullptr};
     if (s) {
         if (s->tol > 0) out.tol = s->tol;
         if (s->tol_mu > 0) out.tol_mu = s->tol_mu;
@@ -193,8 +200,10 @@ int stage_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vecto
     const size_t ns = (size_t)rs * 64;
     std::vector<double> sc(ns * NX, 0.0), sw(ns, 0.0), sE(ns * NX, 0.0);
     std::vector<int32_t> sv(ns, 0), spart(ns, -1);
+    P->stage_slot.assign(D.p, -1);
     for (int r = 0; r < D.p; ++r) {
         const size_t e = (size_t)slot_of[r] * 64 + lane_of[r];
+        P->stage_slot[r] = (int32_t)e;
         if (sv[e]) return fail(CARMPC_EINVAL, "stage layout collision");
         sv[e] = 1;
         if (partner[r] >= 0) spart[e] = slot_of[partner[r]] * 64 + lane_of[partner[r]];
@@ -329,6 +338,7 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
                       M.A[15] == 1.0 && zero_outside(M.B, 4, 2, keepB, 2) && zero_outside(M.Q, 4, 4, keepQ, 4) &&
                       zero_outside(M.R, 2, 2, keepR, 2);
     D.ric = bike ? 2 : 1;
+    P->ric_slot = slot_of;
     *ok = true;
     return CARMPC_OK;
 }
@@ -455,6 +465,12 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     }
     std::vector<int32_t> qp, pre;
     classify(nrm, qp, pre);
+    P->qp_rows = qp;
+    P->pre_rows = pre;
+    P->nrm_all = nrm;
+    P->coef_all_dev = coef;
+    P->stage_all_dev = stage;
+    std::memcpy(P->A_host, d->A, sizeof(double) * NX * NX);
     DevProblem& D = P->dev;
     D.n = n; D.nv = nv; D.p = (int)qp.size(); D.npre = (int)pre.size(); D.ldg = nv + 2; D.N = N; D.nu = nu;
     size_t lds = 0;
@@ -626,6 +642,110 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
         if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
         if (e != hipSuccess) return hipfail(e, "segment launch");
     }
+    return CARMPC_OK;
+}
+
+int carmpc_problem_set_disturbance(carmpc_problem* P, const double* Bd) {
+    if (!P || !Bd) return fail(CARMPC_EINVAL, "null argument");
+    if (!P->assembled || P->dev.nu < 1) return fail(CARMPC_EUNSUPPORTED, "disturbance offsets need an assembled problem");
+    DevProblem& D = P->dev;
+    const int N = D.N, pa = P->p_all;
+    // ABd_k = sum_{m<k} A^m Bd  (mpc.py:631-635)
+    std::vector<double> abd((size_t)(N + 1) * NX, 0.0);
+    double Am[16], acc[NX] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i) Am[i] = (i % 5 == 0) ? 1.0 : 0.0;
+    for (int k = 1; k <= N; ++k) {
+        for (int a = 0; a < NX; ++a)
+            for (int b = 0; b < NX; ++b) acc[a] += Am[a * NX + b] * Bd[b];
+        for (int a = 0; a < NX; ++a) abd[(size_t)k * NX + a] = acc[a];
+        double nx_[16];
+        for (int a = 0; a < NX; ++a)
+            for (int b = 0; b < NX; ++b) {
+                double v = 0.0;
+                for (int c = 0; c < NX; ++c) v += P->A_host[a * NX + c] * Am[c * NX + b];
+                nx_[a * NX + b] = v;
+            }
+        std::memcpy(Am, nx_, sizeof(Am));
+    }
+    std::vector<double> coef((size_t)pa * NX);
+    std::vector<int32_t> stage(pa);
+    if (pa > 0) {
+        HIP_TRY(hipMemcpy(coef.data(), P->coef_all_dev, sizeof(double) * coef.size(), hipMemcpyDeviceToHost), "readback coef");
+        HIP_TRY(hipMemcpy(stage.data(), P->stage_all_dev, sizeof(int32_t) * pa, hipMemcpyDeviceToHost), "readback stage");
+    }
+    std::vector<double> ed_all(pa, 0.0);
+    for (int r = 0; r < pa; ++r)
+        for (int a = 0; a < NX; ++a) ed_all[r] += coef[(size_t)r * NX + a] * abd[(size_t)stage[r] * NX + a];
+    std::vector<double> ed(D.p), pre_ed(D.npre);
+    for (int i = 0; i < D.p; ++i) ed[i] = ed_all[P->qp_rows[i]] / P->nrm_all[P->qp_rows[i]];   // packed rows are normalised
+    for (int i = 0; i < D.npre; ++i) pre_ed[i] = ed_all[P->pre_rows[i]];
+    double *ded, *dpre;
+    HIP_TRY(upload(P, &ded, ed.data(), ed.size()), "upload Ed");
+    HIP_TRY(upload(P, &dpre, pre_ed.data(), pre_ed.size()), "upload pre_Ed");
+    D.Ed = ded;
+    D.pre_Ed = dpre;
+    if (!P->stage_slot.empty()) {
+        std::vector<double> sed((size_t)D.srs * 64, 0.0);
+        for (int i = 0; i < D.p; ++i) sed[P->stage_slot[i]] = ed[i];
+        double* dsed;
+        HIP_TRY(upload(P, &dsed, sed.data(), sed.size()), "upload s_Ed");
+        D.s_Ed = dsed;
+    }
+    if (!P->ric_slot.empty()) {
+        std::vector<double> red((size_t)kRicSlots * kRicLanes, 0.0);
+        for (int i = 0; i < D.p; ++i) red[P->ric_slot[i]] = ed[i];
+        double* dred;
+        HIP_TRY(upload(P, &dred, red.data(), red.size()), "upload r_Ed");
+        D.r_Ed = dred;
+    }
+    return CARMPC_OK;
+}
+
+int carmpc_solve_batch_dist(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref,
+                            const double* dist, double* u_out, int32_t* status, int32_t* iters,
+                            const carmpc_settings* settings, hipStream_t stream) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    if (batch < 0) return fail(CARMPC_EINVAL, "negative batch");
+    if (batch == 0) return CARMPC_OK;
+    if (!x0 || !u_out || !status || !dist) return fail(CARMPC_EINVAL, "null batch pointer");
+    if (!P->dev.Ed) return fail(CARMPC_EINVAL, "no disturbance model: call carmpc_problem_set_disturbance first");
+    Settings s = make_settings(settings);
+    s.dist = dist;
+    int unsupported = 0;
+    hipError_t e = launch_solve(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
+    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+    if (e != hipSuccess) return hipfail(e, "solve launch");
+    return CARMPC_OK;
+}
+
+int carmpc_observer_dist_batch(const carmpc_problem* P, int64_t batch, const double* y, int32_t ny, const double* C,
+                               const double* L1, const double* Cd, const double* L2, const double* Bd, double* xhat,
+                               double* dhat, const double* uprev, int64_t ld_uprev, hipStream_t stream) {
+    if (!P || !y || !C || !L1 || !Cd || !L2 || !Bd || !xhat || !dhat || !uprev) return fail(CARMPC_EINVAL, "null argument");
+    if (!P->assembled) return fail(CARMPC_EINVAL, "observer needs an assembled problem (A, B)");
+    if (ny < 1 || ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
+    thread_local double* dCL = nullptr;
+    thread_local int dev_of = -1;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    constexpr int kStage = 2 * 8 * NX + 8 + 8 + NX;
+    if (!dCL || dev_of != dev) {
+        HIP_TRY(hipMalloc(&dCL, sizeof(double) * kStage), "hipMalloc observer");
+        dev_of = dev;
+    }
+    std::vector<double> host(kStage, 0.0);
+    std::memcpy(host.data(), C, sizeof(double) * ny * NX);
+    std::memcpy(host.data() + 8 * NX, L1, sizeof(double) * NX * ny);
+    std::memcpy(host.data() + 16 * NX, Cd, sizeof(double) * ny);
+    std::memcpy(host.data() + 16 * NX + 8, L2, sizeof(double) * ny);
+    std::memcpy(host.data() + 16 * NX + 16, Bd, sizeof(double) * NX);
+    HIP_TRY(hipMemcpyAsync(dCL, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice, stream), "copy observer");
+    HIP_TRY(hipStreamSynchronize(stream), "sync observer");
+    ObsArgs a{};
+    a.batch = batch; a.ny = ny; a.nu = P->dev.nu; a.ld_uprev = ld_uprev;
+    a.A = P->dev.A; a.B = P->dev.B; a.C = dCL; a.L = dCL + 8 * NX; a.y = y; a.uprev = uprev; a.xhat = xhat;
+    a.Cd = dCL + 16 * NX; a.L2 = dCL + 16 * NX + 8; a.Bd = dCL + 16 * NX + 16; a.dhat = dhat;
+    HIP_TRY(launch_observer(a, stream), "observer launch");
     return CARMPC_OK;
 }
 

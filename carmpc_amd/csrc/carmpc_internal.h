@@ -73,12 +73,20 @@ struct DevProblem {
     const int32_t* r_valid;   // 256
     const int32_t* r_partner; // 256: slot of the opposite row or -1; nullptr when none
     StageMats mats;
+    // constant-disturbance offsets (MPCOutputFBWithDisturbance, mpc.py:631-650): with
+    // x = T x0 + S u + ABd d the rows read w = w0 - E x0 - Ed d.  nullptr until
+    // carmpc_problem_set_disturbance; per layout (packed rows, x0-only rows, slots)
+    const double* Ed;         // p (normalised like w0)
+    const double* pre_Ed;     // npre
+    const double* s_Ed;       // srs*64 (staged slots)
+    const double* r_Ed;       // 256 (Riccati slots)
 };
 
 struct Settings {
     double tol, tol_mu;
     int32_t max_iter;
-    int32_t kernel;   // CARMPC_KERNEL_*: 0 auto (staged when available), 1 dense, 2 staged, 3 dense 4-wave
+    int32_t kernel;        // 0 auto (riccati, staged, dense), 1 dense, 2 staged, 3 dense 4-wave, 4-6 staged A/B, 7 riccati
+    const double* dist;    // per-instance disturbance estimate d (device, batch) or nullptr
 };
 
 
@@ -111,6 +119,9 @@ struct ObsArgs {
     const double* y;
     const double* uprev;
     double* xhat;
+    // disturbance-augmented observer (mpc.py:598-612) when dhat != nullptr
+    const double *Bd, *Cd, *L2;    // device: NX, ny, ny
+    double* dhat;                  // batch
 };
 hipError_t launch_assembly(const AsmArgs& a, hipStream_t s);
 hipError_t launch_pack(const PackArgs& a, hipStream_t s);

@@ -231,11 +231,13 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
             xr[k] = xref ? xref[inst * NX + k] : P.goal[k];
         }
         // ---- x0-only rows (G_r == 0): preconditions on x0 ---------------------
+        const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
         bool bad = false;
         for (int r = lane; r < P.npre; r += 64) {
             double v = P.pre_w0[r];
 #pragma unroll
             for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv[k];
+            if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
             bad |= v < -PRE_TOL;
         }
         if (__any(bad)) {
@@ -261,6 +263,7 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
                 v = P.w0[r];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v -= P.E[r * NX + k] * xv[k];
+                if (P.Ed) v -= P.Ed[r] * dd;
             }
             w[s] = v;
         }

@@ -551,11 +551,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 xr[k] = xref ? xref[inst * NX + k] : P.goal[k];
             }
             // x0-only rows (G_r = 0): preconditions
+            const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
             double bad = 0.0;
             for (int r = j; r < P.npre; r += G16) {
                 double v = P.pre_w0[r];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv0[k];
+                if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
                 bad = v < -PRE_TOL ? 1.0 : bad;
             }
             it = 0;
@@ -574,6 +576,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         v = P.r_w0[e];
 #pragma unroll
                         for (int k = 0; k < NX; ++k) v -= P.r_E[e * NX + k] * xv0[k];
+                        if (P.r_Ed) v -= P.r_Ed[e] * dd;
                     }
                     wv.w[s][lane] = v;
                     bn = fmax(bn, fabs(v));

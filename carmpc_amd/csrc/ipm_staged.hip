@@ -651,11 +651,13 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_staged_kernel(DevProblem P, int
             xv[k] = x0[inst * NX + k];
             xr[k] = xref ? xref[inst * NX + k] : P.goal[k];
         }
+        const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
         bool bad = false;
         for (int r = lane; r < P.npre; r += 64) {
             double v = P.pre_w0[r];
 #pragma unroll
             for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv[k];
+            if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
             bad |= v < -PRE_TOL;
         }
         if (__any(bad)) {
@@ -680,6 +682,7 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_staged_kernel(DevProblem P, int
                 v = P.s_w0[e];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v -= P.s_E[e * NX + k] * xv[k];
+                if (P.s_Ed) v -= P.s_Ed[e] * dd;
             }
             wv.w[s * 64 + lane] = v;
             bn = fmax(bn, fabs(v));

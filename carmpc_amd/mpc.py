@@ -360,3 +360,101 @@ class MPCOutputFB(MPC):
         self.previous_u = u[:self.nu]
         self._u_dev = u_all[:, :self.nu].contiguous()
         return u[:self.nu]
+
+
+class MPCOutputFBWithDisturbance(MPC):
+    """Output-feedback MPC with a constant scalar disturbance d (mpc.py:495-667):
+        x+ = A x + B u + Bd d,   y = C x + Cd d,
+    a disturbance-augmented Luenberger observer, and the QP of MPCStateFB with the predicted
+    states shifted by ABd d (x = T x0 + S u + ABd d, mpc.py:631-650).  Observer and QP run on
+    the GPU (carmpc_observer_dist_batch, carmpc_solve_batch_dist)."""
+
+    C_OUT = MPCOutputFB.C_OUT
+    BD = np.array([1.0, 1.0, 1.0, 1.0])       # mpc.py:536 (the value the constructor leaves)
+    CD = np.array([1.0, 1.0, 1.0])            # mpc.py:537
+    L1_GAIN = MPCOutputFB.L_GAIN              # mpc.py:541-544
+    L2_GAIN = np.array([1.0, 1.0, 1.0])       # mpc.py:546
+    X_REF = np.array([30.0, 1.5, 0.0, 0.0])   # mpc.py:624 (target selection commented out in step)
+
+    def __init__(self, dt: float, N: int, lin_state: ArrayLike, lin_input: ArrayLike, init_state: ArrayLike,
+                 terminal_constraint: bool = True, input_constraint: bool = True, state_constraint: bool = True,
+                 env: BaseEnv = None, **kw) -> None:
+        super().__init__(dt, N, lin_state, lin_input, terminal_constraint, input_constraint, state_constraint,
+                         env, **kw)
+        self.C = self.C_OUT.copy()
+        self.Bd = self.BD.copy()
+        self.Cd = self.CD.copy()
+        self.C_hat = np.hstack((self.C, self.Cd.reshape(-1, 1)))                                   # mpc.py:538
+        self.L1 = self.L1_GAIN.copy()
+        self.L2 = self.L2_GAIN.copy()
+        self.A_hat = np.vstack((np.hstack((self.A, self.Bd.reshape(-1, 1))),
+                                np.array([0, 0, 0, 0, 1]).reshape(1, -1)))                       # mpc.py:548
+        self.B_hat = np.vstack((self.B, [0, 0]))                                                 # mpc.py:549
+        self.x_estimate = np.array(init_state, dtype=float)
+        self.d_estimate = 0.0
+        self.previous_u = np.zeros(2)
+        self.y_goal = self.C @ env.goal                                                          # mpc.py:567
+        self._dist_ready = False
+        self.check_constraints()
+
+    def _qp_dist(self):
+        qp = self.qp
+        if not self._dist_ready:
+            qp.set_disturbance(self.Bd)
+            self._dist_ready = True
+        return qp
+
+    def optimal_target_selection(self) -> tuple:
+        """(x_ref, u_ref) with the disturbance (mpc.py:572-596): the equality block
+        [[I-A, -B], [C, 0]] [x; u] = [Bd d; y_goal - Cd d] has full column rank for the Road*
+        setups, so the feasible set is one point; solved in closed form (not called by step,
+        as in the reference)."""
+        M = np.block([[np.eye(self.nx) - self.A, -self.B], [self.C, np.zeros((self.C.shape[0], self.nu))]])
+        rhs = np.concatenate((self.Bd * self.d_estimate, self.y_goal - self.Cd * self.d_estimate))
+        if np.linalg.matrix_rank(M) < self.nx + self.nu:
+            raise NotImplementedError("target selection with a non-unique equality solution")
+        xu, *_ = np.linalg.lstsq(M, rhs, rcond=None)
+        if np.abs(M @ xu - rhs).max() > 1e-9:
+            raise OutsideTheRegionOfAttractionError("no steady state reaches y_goal")
+        return xu[:self.nx], xu[self.nx:]
+
+    def luenberger_observer(self, y0) -> tuple:
+        """Host form of the disturbance observer (mpc.py:598-612, without its debug prints):
+        e = y - C x_hat - Cd d_hat; x_hat+ = A x_hat + Bd d_hat + B u_prev + L1 e; d_hat+ = d_hat + L2 . e.
+        ``step`` runs the same update on the GPU."""
+        e = np.asarray(y0, float) - self.C @ self.x_estimate - self.Cd * self.d_estimate
+        x_new = self.A @ self.x_estimate + self.Bd * self.d_estimate + self.B @ self.previous_u + self.L1 @ e
+        return x_new, float(self.d_estimate + self.L2 @ e)
+
+    def step_batch(self, y, xhat, dhat, uprev):
+        """Observer + QP for a batch on the GPU: y (B x 3), xhat (B x 4), dhat (B,), uprev (B x 2)
+        device float64 tensors; xhat and dhat are updated in place.
+        Returns (u0 (B x nu), u (B x N nu), status (B,))."""
+        import torch
+        qp = self._qp_dist()
+        qp.observe_dist(y, xhat, dhat, uprev, self.C, self.L1, self.Cd, self.L2, self.Bd)
+        Rf = torch.as_tensor(self.X_REF, dtype=torch.float64, device=qp.device).expand(xhat.shape[0], 4).contiguous()
+        u, st, _ = qp.solve(xhat, Rf, self.settings, dist=dhat)
+        return u[:, :self.nu], u, st
+
+    def step(self, y0) -> np.ndarray:
+        """Observer -> QP with the disturbance offset (mpc.py:614-667), both on the GPU."""
+        import torch
+        qp = self._qp_dist()
+        dev = qp.device
+        xh = torch.as_tensor(self.x_estimate.reshape(1, 4)).to(dev).contiguous()
+        dh = torch.tensor([float(self.d_estimate)], dtype=torch.float64, device=dev)
+        up = torch.as_tensor(np.asarray(self.previous_u, dtype=np.float64).reshape(1, -1)).to(dev)
+        y = torch.as_tensor(np.asarray(y0, dtype=np.float64).reshape(1, -1)).to(dev)
+        _, u_all, st = self.step_batch(y, xh, dh, up)
+        x0 = xh[0].cpu().numpy()
+        self.x_estimate = x0.copy()
+        self.d_estimate = float(dh.cpu()[0])
+        u = self._check_status(int(st.cpu()[0]), u_all[0].cpu().numpy())
+        m = self._mats()
+        dx = x0 - self.X_REF
+        self.x_horizon = (m["T"] @ dx + m["S"] @ u).reshape(-1, self.nx) + self.goal     # mpc.py:659-660
+        self.u_horizon = u.reshape(-1, 2)
+        self.cost = 0.5 * u @ m["H"] @ u + (m["h"] @ dx) @ u                            # mpc.py:639,653
+        self.previous_u = u[:self.nu]
+        return u[:self.nu]

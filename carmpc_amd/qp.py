@@ -158,14 +158,31 @@ class QPProblem:
         return float(_native.load().carmpc_executed_flops_per_iter(self._h, kernel))
 
     # ----------------------------------------------------------------- solve
+    def set_disturbance(self, Bd) -> None:
+        """Constant scalar disturbance model x+ = A x + B u + Bd d (mpc.py:508-512): stores the row
+        offsets of x = T x0 + S u + ABd d (mpc.py:631-650) for ``solve(..., dist=d)``."""
+        Bd = _f64(Bd).reshape(-1)
+        if Bd.shape != (NX,):
+            raise ValueError("Bd must have nx entries")
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_problem_set_disturbance(self._h, _dptr(Bd)), "carmpc_problem_set_disturbance")
+        self.Bd = Bd.copy()
+
     def solve(self, x0: torch.Tensor, xref: torch.Tensor | None = None, settings: SolverSettings | None = None,
-              out: tuple | None = None, stream=None):
+              out: tuple | None = None, stream=None, dist: torch.Tensor | None = None):
         """Solve QP(x0) for every row of x0 (B x 4, float64, on this problem's device).
+        ``dist`` (B,) per-instance disturbance estimates (needs ``set_disturbance``).
 
         Returns (u (B x n) float64, status (B,) int32, iters (B,) int32), all on device;
         stream-ordered, no host synchronisation."""
         x0 = _as_dev(x0, self.device)
         B = x0.shape[0]
+        if dist is not None:
+            if not isinstance(dist, torch.Tensor):
+                dist = torch.as_tensor(np.asarray(dist, dtype=np.float64))
+            dist = dist.reshape(-1).to(device=self.device, dtype=torch.float64).contiguous()
+            if dist.shape[0] != B:
+                raise ValueError("dist must have one entry per instance")
         if xref is not None:
             xref = _as_dev(xref, self.device)
             if xref.shape != x0.shape:
@@ -178,9 +195,14 @@ class QPProblem:
             u, st, it = out
         s = (settings or SolverSettings()).c()
         with torch.cuda.device(self.device):
-            check(_native.load().carmpc_solve_batch(self._h, B, _tptr(x0), _tptr(xref), _tptr(u), _tptr(st),
-                                                    _tptr(it), ctypes.byref(s), _stream_handle(stream)),
-                  "carmpc_solve_batch")
+            if dist is None:
+                check(_native.load().carmpc_solve_batch(self._h, B, _tptr(x0), _tptr(xref), _tptr(u), _tptr(st),
+                                                        _tptr(it), ctypes.byref(s), _stream_handle(stream)),
+                      "carmpc_solve_batch")
+            else:
+                check(_native.load().carmpc_solve_batch_dist(self._h, B, _tptr(x0), _tptr(xref), _tptr(dist), _tptr(u),
+                                                             _tptr(st), _tptr(it), ctypes.byref(s),
+                                                             _stream_handle(stream)), "carmpc_solve_batch_dist")
         return u, st, it
 
     def observe(self, y: torch.Tensor, xhat: torch.Tensor, uprev: torch.Tensor, C, L, stream=None) -> None:
@@ -195,6 +217,24 @@ class QPProblem:
             check(_native.load().carmpc_observer_batch(self._h, xhat.shape[0], _tptr(y), C.shape[0], _dptr(C),
                                                        _dptr(L), _tptr(xhat), _tptr(uprev), uprev.stride(0),
                                                        _stream_handle(stream)), "carmpc_observer_batch")
+
+
+    def observe_dist(self, y: torch.Tensor, xhat: torch.Tensor, dhat: torch.Tensor, uprev: torch.Tensor,
+                     C, L1, Cd, L2, Bd, stream=None) -> None:
+        """In-place disturbance-augmented observer (mpc.py:598-612): e = y - C xhat - Cd dhat,
+        xhat <- A xhat + Bd dhat + B uprev + L1 e, dhat <- dhat + L2 . e."""
+        C, L1, Cd, L2, Bd = _f64(C), _f64(L1), _f64(Cd).reshape(-1), _f64(L2).reshape(-1), _f64(Bd).reshape(-1)
+        y = _as_dev(y, self.device, width=C.shape[0])
+        for t, nm in ((xhat, "xhat"), (dhat, "dhat")):
+            if t.dtype != torch.float64 or not t.is_contiguous() or t.device != self.device:
+                raise ValueError(f"{nm} must be a contiguous float64 tensor on the problem device")
+        if uprev.dtype != torch.float64 or uprev.stride(1) != 1:
+            raise ValueError("uprev must be float64 with unit column stride")
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_observer_dist_batch(self._h, xhat.shape[0], _tptr(y), C.shape[0], _dptr(C),
+                                                            _dptr(L1), _dptr(Cd), _dptr(L2), _dptr(Bd), _tptr(xhat),
+                                                            _tptr(dhat), _tptr(uprev), uprev.stride(0),
+                                                            _stream_handle(stream)), "carmpc_observer_dist_batch")
 
 
 def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,

@@ -10,6 +10,9 @@
  *   MPCStateFB.step  cp.Problem(...).solve()   lib/mpc.py:318-335  -> carmpc_solve_batch
  *   MPCOutputFB.step cp.Problem(...).solve()   lib/mpc.py:461-478  -> carmpc_solve_batch
  *   MPCOutputFB.luenberger_observer            lib/mpc.py:439-448  -> carmpc_observer_batch
+ *   MPCOutputFBWithDisturbance.step            lib/mpc.py:614-667  -> carmpc_solve_batch_dist
+ *     ABd offsets of the constraints           lib/mpc.py:631-650  -> carmpc_problem_set_disturbance
+ *   MPCOutputFBWithDisturbance.luenberger_observer lib/mpc.py:598-612 -> carmpc_observer_dist_batch
  *   OutsideTheRegionOfAttractionError          lib/mpc.py:17,336-338 -> status CARMPC_PRIMAL_INFEASIBLE
  *   CarSimulator.step (plant)                  lib/simulator.py:51-69,99-118 -> carmpc_plant_step_batch
  *
@@ -139,6 +142,22 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
                           const double* x0, const double* xref, double* u_out, int64_t ld_u,
                           int32_t* status, int32_t* iters, const carmpc_settings* settings,
                           hipStream_t stream);
+
+/* MPCOutputFBWithDisturbance (mpc.py:495-667): constant scalar disturbance d with
+ * x+ = A x + B u + Bd d.  set_disturbance stores the row offsets Ed (x = T x0 + S u + ABd d,
+ * ABd_k = sum_{m<k} A^m Bd, mpc.py:631-637); solve_batch_dist then solves the QPs with
+ * w = w0 - E x0 - Ed d_b for per-instance device estimates dist[b]. */
+int carmpc_problem_set_disturbance(carmpc_problem* prob, const double* Bd /* NX, host */);
+int carmpc_solve_batch_dist(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
+                            const double* dist, double* u_out, int32_t* status, int32_t* iters,
+                            const carmpc_settings* settings, hipStream_t stream);
+/* Disturbance-augmented Luenberger observer (mpc.py:598-612), in place on device:
+ * e = y - C xhat - Cd dhat; xhat <- A xhat + Bd dhat + B uprev + L1 e; dhat <- dhat + L2 . e.
+ * C (ny x NX), L1 (NX x ny), Cd, L2 (ny), Bd (NX) are host arrays. */
+int carmpc_observer_dist_batch(const carmpc_problem* prob, int64_t batch, const double* y, int32_t ny,
+                               const double* C, const double* L1, const double* Cd, const double* L2,
+                               const double* Bd, double* xhat, double* dhat, const double* uprev,
+                               int64_t ld_uprev, hipStream_t stream);
 
 /* Luenberger observer (mpc.py:439-448), in place on device:
  *   xhat <- A xhat + B uprev + L (y - C xhat)

@@ -284,6 +284,51 @@ def optimal_target_selection(A, B, y_goal, C=C_OUT):
     return xu[:4], xu[4:]
 
 
+# --- lib/mpc.py:495-667 (MPCOutputFBWithDisturbance) --------------------------
+# x+ = A x + B u + Bd d,  y = C x + Cd d, d a scalar disturbance (mpc.py:508-512); the
+# constants below are the values the constructor leaves in place (the second assignments,
+# mpc.py:536-537), the observer gains of mpc.py:541-546 and the hard-coded reference of
+# step() (mpc.py:624: the target selection call is commented out there).
+BD_DIST = np.array([1.0, 1.0, 1.0, 1.0])                       # mpc.py:536
+CD_DIST = np.array([1.0, 1.0, 1.0])                            # mpc.py:537
+L1_DIST = L_OBS.copy()                                         # mpc.py:541-544
+L2_DIST = np.array([1.0, 1.0, 1.0])                            # mpc.py:546
+XREF_DIST = np.array([30.0, 1.5, 0.0, 0.0])                    # mpc.py:624
+
+
+def disturbance_observer(A, B, x_est, d_est, u_prev, y0, C=C_OUT, Bd=BD_DIST, Cd=CD_DIST, L1=L1_DIST,
+                         L2=L2_DIST):
+    """(x_hat+, d_hat+) of the disturbance-augmented Luenberger observer.  Restates
+    mpc.py:598-612 (without its debug prints): innovation e = y - C x_hat - Cd d_hat,
+    x_hat+ = A x_hat + Bd d_hat + B u_prev + L1 e,  d_hat+ = d_hat + L2 . e."""
+    e = np.asarray(y0, float) - C @ x_est - Cd * d_est
+    return A @ x_est + Bd * d_est + B @ u_prev + L1 @ e, float(d_est + L2 @ e)
+
+
+def abd_offsets(A, Bd, N):
+    """ABd_k = sum_{m<k} A^m Bd, k = 0..N: the predicted-state offset of a constant
+    disturbance, x = T x0 + S u + ABd d (mpc.py:631-637)."""
+    out = np.zeros((N + 1, 4))
+    acc = np.zeros(4)
+    Am = np.eye(4)
+    for k in range(1, N + 1):
+        acc = acc + Am @ Bd
+        Am = A @ Am
+        out[k] = acc
+    return out
+
+
+def qp_data_dist(asm: Assembly, x0, d, xref=XREF_DIST, Bd=BD_DIST):
+    """Per-instance QP vectors of MPCOutputFBWithDisturbance.step (mpc.py:630-650):
+    q = h (x0 - xref), w = w0 - E x0 - (rows . ABd_k) d (constraints act on x with the offset)."""
+    x0 = np.asarray(x0, float)
+    q = asm.h @ (x0 - np.asarray(xref, float))
+    abd = abd_offsets(asm.A, Bd, asm.N)
+    Ed = np.einsum("ra,ra->r", asm.row_coef, abd[asm.row_stage]) if len(asm.w0) else np.zeros(0)
+    w = asm.w0 - asm.E @ x0 - Ed * float(d)
+    return q, w, Ed
+
+
 # --- lib/simulator.py:51-69,83-118 (plant) ------------------------------------
 def plant_step(state, u, dt=DT_SIMULATION, l1=L1):
     """Forward-Euler kinematic bicycle.  Restates simulator.py:51-69."""

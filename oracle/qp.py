@@ -351,3 +351,31 @@ def solve_instance(asm, x0, xref=None, info=None, **kw):
     else:
         out.update(u_exact=None, certified=False)
     return out
+
+
+def solve_instance_dist(asm, x0, d, xref=None, Bd=None, **kw):
+    """Oracle for MPCOutputFBWithDisturbance.step's QP (mpc.py:630-656): the rows read
+    w = w0 - E x0 - Ed d with Ed_r = c_r . ABd_{k_r} (assembly.qp_data_dist), the cost uses
+    x0 - xref.  Same preconditions / normalisation / IPM / certificate as solve_instance."""
+    from .assembly import BD_DIST, XREF_DIST, qp_data_dist
+    xref = XREF_DIST if xref is None else xref
+    q, w, Ed = qp_data_dist(asm, x0, d, xref, BD_DIST if Bd is None else Bd)
+    nrm = np.linalg.norm(asm.G, axis=1) if asm.G.size else np.zeros(len(asm.w0))
+    thr = ZERO_ROW * (nrm.max() if nrm.size else 0.0)
+    keep = nrm > thr
+    Gn, w0n, En, _, _, _ = normalize_rows(asm.G, asm.w0, asm.E)
+    wn = w[keep] / nrm[keep]
+    out = dict(q=q, w=wn)
+    pre = w[~keep]
+    if pre.size and pre.min() < -PRE_TOL:
+        out.update(status=STATUS_INFEASIBLE, iters=0, u=np.zeros(len(q)), u_exact=None, certified=False)
+        return out
+    kw.setdefault("partner", opposite_pairs(Gn, w0n, En))
+    u, st, it, _ = ipm(asm.H, q, Gn, wn, asm.lb, asm.ub, **kw)
+    out.update(status=st, iters=it, u=u)
+    if st == STATUS_OPTIMAL:
+        ue, ok, res = certify(asm.H, q, Gn, wn, asm.lb, asm.ub, u)
+        out.update(u_exact=ue, certified=ok, kkt=res)
+    else:
+        out.update(u_exact=None, certified=False)
+    return out
