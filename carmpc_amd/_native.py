@@ -25,7 +25,12 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_observer_batch", "carmpc_plant_step_batch", "carmpc_canonical_flops_per_iter",
            "carmpc_last_error", "carmpc_version", "carmpc_problem_kernel",
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
-           "carmpc_observer_dist_batch")
+           "carmpc_observer_dist_batch", "carmpc_closed_loop_batch")
+
+# outcomes of carmpc_closed_loop_batch (carmpc.h)
+LOOP_RUNNING, LOOP_REACHED, LOOP_INFEASIBLE, LOOP_INPUT_VIOLATION, LOOP_TIMEOUT, LOOP_SOLVER_FAILURE = -1, 0, 1, 2, 3, 4
+LOOP_NAMES = {LOOP_RUNNING: "running", LOOP_REACHED: "reached", LOOP_INFEASIBLE: "infeasible",
+              LOOP_INPUT_VIOLATION: "input_violation", LOOP_TIMEOUT: "timeout", LOOP_SOLVER_FAILURE: "solver_failure"}
 
 
 class CarMPCNativeError(RuntimeError):
@@ -40,6 +45,15 @@ class ModelDesc(ctypes.Structure):
                 ("n_state_rows", ctypes.c_int32), ("state_A", _dp), ("state_b", _dp),
                 ("n_term_rows", ctypes.c_int32), ("term_A", _dp), ("term_b", _dp),
                 ("u_lower", _dp), ("u_upper", _dp), ("goal", _dp)]
+
+
+class LoopDesc(ctypes.Structure):
+    """carmpc_loop_desc (include/carmpc.h)."""
+    _dp = ctypes.POINTER(ctypes.c_double)
+    _fields_ = [("mode", ctypes.c_int32), ("steps_update", ctypes.c_int32), ("last_step", ctypes.c_int32),
+                ("ny", ctypes.c_int32), ("dt", ctypes.c_double), ("l1", ctypes.c_double),
+                ("goal_tol", ctypes.c_double), ("goal", _dp), ("C", _dp), ("L", _dp), ("Cd", _dp), ("L2", _dp),
+                ("Bd", _dp)]
 
 
 class Settings(ctypes.Structure):
@@ -82,6 +96,8 @@ def load():
         "carmpc_problem_set_disturbance": ([vp, dp], ctypes.c_int),
         "carmpc_solve_batch_dist": ([vp, i64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_observer_dist_batch": ([vp, i64, vp, i32, dp, dp, dp, dp, dp, vp, vp, vp, i64, vp], ctypes.c_int),
+        "carmpc_closed_loop_batch": ([vp, i64, ctypes.POINTER(LoopDesc), vp, vp, vp, vp, vp, vp, vp, i32,
+                                      ctypes.POINTER(Settings), vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -718,6 +718,92 @@ int carmpc_solve_batch_dist(const carmpc_problem* P, int64_t batch, const double
     return CARMPC_OK;
 }
 
+int carmpc_closed_loop_batch(const carmpc_problem* P, int64_t batch, const carmpc_loop_desc* L, double* state,
+                             double* xhat, double* dhat, const double* xref, double* u, int32_t* outcome,
+                             int32_t* steps, int32_t check_every, const carmpc_settings* settings,
+                             hipStream_t stream) {
+    if (!P || !L) return fail(CARMPC_EINVAL, "null argument");
+    if (batch < 0 || batch > INT32_MAX) return fail(CARMPC_EINVAL, "batch out of range");
+    if (batch == 0) return CARMPC_OK;
+    if (!state || !u || !outcome || !steps) return fail(CARMPC_EINVAL, "null batch pointer");
+    if (!P->assembled || P->dev.nu != 2) return fail(CARMPC_EUNSUPPORTED, "closed loop needs an assembled problem with nu = 2");
+    if (L->mode < 0 || L->mode > 2) return fail(CARMPC_EINVAL, "mode must be 0, 1 or 2");
+    if (L->steps_update < 1 || L->last_step < 0 || !(L->dt > 0.0) || !(L->l1 > 0.0))
+        return fail(CARMPC_EINVAL, "steps_update >= 1, last_step >= 0, dt > 0, l1 > 0 required");
+    if (L->mode >= 1) {
+        if (!xhat || !L->C || !L->L) return fail(CARMPC_EINVAL, "output feedback needs xhat, C and L");
+        if (L->ny < 1 || L->ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
+    }
+    if (L->mode == 2) {
+        if (!dhat || !L->Cd || !L->L2 || !L->Bd) return fail(CARMPC_EINVAL, "disturbance mode needs dhat, Cd, L2, Bd");
+        if (!P->dev.Ed) return fail(CARMPC_EINVAL, "no disturbance model: call carmpc_problem_set_disturbance first");
+    }
+    const int64_t n = P->dev.n;
+    // loop constants: C 8*NX | L NX*8 | Cd 8 | L2 8 | Bd NX | goal NX
+    constexpr int kC = 0, kL = 8 * NX, kCd = 16 * NX, kL2 = 16 * NX + 8, kBd = 16 * NX + 16, kGoal = 17 * NX + 16,
+                  kConst = 18 * NX + 16;
+    std::vector<double> host(kConst, 0.0);
+    const int ny = L->mode >= 1 ? L->ny : 0;
+    if (ny) {
+        std::memcpy(host.data() + kC, L->C, sizeof(double) * ny * NX);
+        std::memcpy(host.data() + kL, L->L, sizeof(double) * NX * ny);
+    }
+    if (L->mode == 2) {
+        std::memcpy(host.data() + kCd, L->Cd, sizeof(double) * ny);
+        std::memcpy(host.data() + kL2, L->L2, sizeof(double) * ny);
+        std::memcpy(host.data() + kBd, L->Bd, sizeof(double) * NX);
+    }
+    HIP_TRY(hipMemcpy(host.data() + kGoal, P->dev.goal, sizeof(double) * NX, hipMemcpyDeviceToHost), "read goal");
+    if (L->goal) std::memcpy(host.data() + kGoal, L->goal, sizeof(double) * NX);
+    // workspace: constants, QP status, two slot lists and their counts (stream-ordered)
+    const size_t bytes = sizeof(double) * kConst + sizeof(int32_t) * (3 * (size_t)batch + 2);
+    void* ws = nullptr;
+    HIP_TRY(hipMallocAsync(&ws, bytes, stream), "hipMallocAsync loop workspace");
+    double* dconst = static_cast<double*>(ws);
+    int32_t* ibase = reinterpret_cast<int32_t*>(dconst + kConst);
+    hipError_t e = hipMemcpyAsync(dconst, host.data(), sizeof(double) * kConst, hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);   // host staging buffer goes out of scope
+    LoopArgs a{};
+    a.batch = batch; a.mode = L->mode; a.ny = ny; a.steps_update = L->steps_update; a.last_step = L->last_step;
+    a.ld_u = n; a.dt = L->dt; a.l1 = L->l1; a.goal_tol = L->goal_tol;
+    a.A = P->dev.A; a.B = P->dev.B;
+    a.C = dconst + kC; a.L = dconst + kL; a.Cd = dconst + kCd; a.L2 = dconst + kL2; a.Bd = dconst + kBd;
+    a.goal = dconst + kGoal;
+    a.state = state; a.xhat = xhat; a.dhat = dhat; a.u = u;
+    int32_t* qp_status = ibase;
+    a.qp_status = qp_status;
+    a.outcome = outcome; a.steps = steps;
+    a.idx_cur = ibase + batch; a.idx_next = ibase + 2 * batch;
+    a.cnt_cur = ibase + 3 * batch; a.cnt_next = ibase + 3 * batch + 1;
+    if (e == hipSuccess) e = launch_loop_init(a, stream);
+    Settings s = make_settings(settings);
+    if (L->mode == 2) s.dist = dhat;
+    const double* x_qp = L->mode == 0 ? state : xhat;
+    int unsupported = 0;
+    for (int32_t i = 0; i <= L->last_step && e == hipSuccess; ++i) {
+        e = launch_loop_advance(a, i, stream);
+        if (e == hipSuccess && i % L->steps_update == 0) {
+            s.index = a.idx_cur;
+            s.count = a.cnt_cur;
+            e = launch_solve(P->dev, batch, x_qp, xref, u, n, qp_status, nullptr, s, stream, &unsupported);
+        }
+        if (e == hipSuccess) e = launch_loop_finish(a, i, stream);
+        std::swap(a.idx_cur, a.idx_next);
+        std::swap(a.cnt_cur, a.cnt_next);
+        if (e == hipSuccess && check_every > 0 && (i + 1) % check_every == 0 && i < L->last_step) {
+            int32_t left = 0;
+            e = hipMemcpyAsync(&left, a.cnt_cur, sizeof(int32_t), hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            if (e == hipSuccess && left == 0) break;
+        }
+    }
+    const hipError_t ef = hipFreeAsync(ws, stream);
+    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+    if (e != hipSuccess) return hipfail(e, "closed loop");
+    if (ef != hipSuccess) return hipfail(ef, "hipFreeAsync loop workspace");
+    return CARMPC_OK;
+}
+
 int carmpc_observer_dist_batch(const carmpc_problem* P, int64_t batch, const double* y, int32_t ny, const double* C,
                                const double* L1, const double* Cd, const double* L2, const double* Bd, double* xhat,
                                double* dhat, const double* uprev, int64_t ld_uprev, hipStream_t stream) {

@@ -87,6 +87,8 @@ struct Settings {
     int32_t max_iter;
     int32_t kernel;        // 0 auto (riccati, staged, dense), 1 dense, 2 staged, 3 dense 4-wave, 4-6 staged A/B, 7 riccati
     const double* dist;    // per-instance disturbance estimate d (device, batch) or nullptr
+    const int32_t* index;  // slot -> instance row (device) or nullptr = identity
+    const int32_t* count;  // number of slots (device scalar) or nullptr = batch
 };
 
 
@@ -123,6 +125,23 @@ struct ObsArgs {
     const double *Bd, *Cd, *L2;    // device: NX, ny, ny
     double* dhat;                  // batch
 };
+// Closed-loop runner (closed_loop.hip): one launch pair per loop index around the QP launch.
+struct LoopArgs {
+    int64_t batch;
+    int32_t mode, ny, steps_update, last_step;
+    int64_t ld_u;
+    double dt, l1, goal_tol;
+    const double *A, *B;                 // device, from the problem
+    const double *C, *L, *Cd, *L2, *Bd;  // device copies of the observer data (modes 1, 2)
+    const double* goal;                  // device NX
+    double *state, *xhat, *dhat, *u;     // B*NX, B*NX, B, B*ld_u
+    const int32_t* qp_status;            // B
+    int32_t *outcome, *steps;            // B
+    int32_t *idx_cur, *cnt_cur, *idx_next, *cnt_next;
+};
+hipError_t launch_loop_init(const LoopArgs& a, hipStream_t s);
+hipError_t launch_loop_advance(const LoopArgs& a, int32_t i, hipStream_t s);
+hipError_t launch_loop_finish(const LoopArgs& a, int32_t i, hipStream_t s);
 hipError_t launch_assembly(const AsmArgs& a, hipStream_t s);
 hipError_t launch_pack(const PackArgs& a, hipStream_t s);
 hipError_t launch_observer(const ObsArgs& a, hipStream_t s);

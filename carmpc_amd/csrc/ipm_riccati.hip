@@ -513,8 +513,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     // next instance at the first trip after finishing one, so the 4 groups of a wave never
     // wait for the slowest instance (infeasible ones stop after a few iterations).
     const int64_t stride = (int64_t)gridDim.x * WPB * 4;
-    int64_t inst = ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
-    bool live = inst < batch;   // the group has an instance to work on
+    // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
+    const int64_t nlive = S.count ? (int64_t)*S.count : batch;
+    int64_t slot = ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
+    bool live = slot < nlive;   // the group has an instance to work on
+    int64_t inst = live && S.index ? (int64_t)S.index[slot] : slot;
     bool fresh = true;          // ... that still needs its initial point
     double s_[RS], z_[RS], ra[RS];
     double xs[2][4];
@@ -534,8 +537,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             status_out[inst] = st;
             if (iters_out) iters_out[inst] = it;
         }
-        inst += stride;
-        live = inst < batch;
+        slot += stride;
+        live = slot < nlive;
+        inst = live && S.index ? (int64_t)S.index[slot] : slot;
         fresh = true;
     };
     RT_DECL

@@ -644,7 +644,10 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_staged_kernel(DevProblem P, int
     const int m_rows = p + (P.boxed ? 2 * NV : 0);
     const double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
 
-    for (int64_t inst = (int64_t)blockIdx.x * kWPB + wave; inst < batch; inst += (int64_t)gridDim.x * kWPB) {
+    // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
+    const int64_t nlive = S.count ? (int64_t)*S.count : batch;
+    for (int64_t slot = (int64_t)blockIdx.x * kWPB + wave; slot < nlive; slot += (int64_t)gridDim.x * kWPB) {
+        const int64_t inst = S.index ? (int64_t)S.index[slot] : slot;
         double xv[NX], xr[NX];
 #pragma unroll
         for (int k = 0; k < NX; ++k) {

@@ -237,6 +237,50 @@ class QPProblem:
                                                             _stream_handle(stream)), "carmpc_observer_dist_batch")
 
 
+    def closed_loop(self, state: torch.Tensor, *, mode: int = 0, steps_update: int = 1, last_step: int = 151,
+                    dt: float = 0.2, l1: float = 3.5, goal_tol: float = 0.1, goal=None,
+                    xhat: torch.Tensor | None = None, dhat: torch.Tensor | None = None,
+                    xref: torch.Tensor | None = None, C=None, L=None, Cd=None, L2=None, Bd=None,
+                    settings: SolverSettings | None = None, check_every: int = 8, stream=None) -> dict:
+        """Run the examples' runner loop for every row of ``state`` on the GPU
+        (carmpc_closed_loop_batch): mode 0 state feedback, 1 output feedback (xhat, C, L),
+        2 output feedback with disturbance (also dhat, Cd, L2, Bd; needs set_disturbance).
+        ``state``, ``xhat`` and ``dhat`` are updated in place.  Returns a dict of device tensors
+        {state, xhat, dhat, u (last QP solution), outcome, steps}."""
+        for t, nm in ((state, "state"), (xhat, "xhat"), (dhat, "dhat")):
+            if t is not None and (t.dtype != torch.float64 or not t.is_contiguous() or t.device != self.device):
+                raise ValueError(f"{nm} must be a contiguous float64 tensor on the problem device")
+        if state.dim() != 2 or state.shape[1] != NX:
+            raise ValueError("state must be B x 4")
+        B = state.shape[0]
+        if xhat is not None and tuple(xhat.shape) != (B, NX):
+            raise ValueError("xhat must be B x 4")
+        if dhat is not None and dhat.numel() != B:
+            raise ValueError("dhat must have one entry per instance")
+        if xref is not None:
+            xref = _as_dev(xref, self.device)
+            if xref.shape[0] == 1 and B > 1:
+                xref = xref.expand(B, NX).contiguous()
+            if tuple(xref.shape) != (B, NX):
+                raise ValueError("xref must be B x 4 (or 1 x 4)")
+        C, L, Cd, L2, Bd = _f64(C), _f64(L), _f64(Cd), _f64(L2), _f64(Bd)
+        goal = _f64(goal)
+        desc = _native.LoopDesc(mode, steps_update, last_step, 0 if C is None else C.shape[0], dt, l1, goal_tol,
+                                _dptr(goal), _dptr(C), _dptr(L), _dptr(None if Cd is None else Cd.reshape(-1)),
+                                _dptr(None if L2 is None else L2.reshape(-1)),
+                                _dptr(None if Bd is None else Bd.reshape(-1)))
+        keep = (C, L, Cd, L2, Bd, goal)   # noqa: F841  (host arrays live through the call)
+        u = torch.empty((B, self.n), dtype=torch.float64, device=self.device)
+        outcome = torch.empty(B, dtype=torch.int32, device=self.device)
+        steps = torch.empty(B, dtype=torch.int32, device=self.device)
+        s = (settings or SolverSettings()).c()
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_closed_loop_batch(self._h, B, ctypes.byref(desc), _tptr(state), _tptr(xhat),
+                                                          _tptr(dhat), _tptr(xref), _tptr(u), _tptr(outcome),
+                                                          _tptr(steps), check_every, ctypes.byref(s),
+                                                          _stream_handle(stream)), "carmpc_closed_loop_batch")
+        return {"state": state, "xhat": xhat, "dhat": dhat, "u": u, "outcome": outcome, "steps": steps}
+
 def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,
                    settings: SolverSettings | None = None, stream=None):
     """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j]."""

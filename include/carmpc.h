@@ -174,6 +174,49 @@ int carmpc_observer_batch(const carmpc_problem* prob, int64_t batch, const doubl
 int carmpc_plant_step_batch(int64_t batch, double* state, const double* u, int64_t ld_u, double dt,
                             double l1, int32_t* bad, hipStream_t stream);
 
+/* ---- closed loop on the device -------------------------------------
+ * The examples' runner loops for B independent cars, entirely on the GPU:
+ *   examples/run_MPCStateFB.py:26-43   mode 0: u = controller.step(state)
+ *   examples/run_MPCOutputFB.py:28-50  mode 1: u = controller.step(C state) (Luenberger, mpc.py:439-492)
+ *   MPCOutputFBWithDisturbance         mode 2: observer mpc.py:598-612 + ABd offsets (needs
+ *                                      carmpc_problem_set_disturbance)
+ * Per loop index i = 0, 1, ...: check_input(u) (simulator.py:83-97, clip=False), plant step
+ * (simulator.py:51-69,99-118), every steps_update-th index the controller step (observer + QP),
+ * then the runner's stop tests: QP infeasible -> OutsideTheRegionOfAttractionError; all
+ * |x - goal| <= goal_tol (goal_tol <= 0: no goal test); i >= last_step.
+ * The reference loop is the special case batch = 1. */
+enum {
+    CARMPC_LOOP_RUNNING = -1,
+    CARMPC_LOOP_REACHED = 0,          /* goal test passed (run_MPCStateFB.py:40)              */
+    CARMPC_LOOP_INFEASIBLE = 1,       /* QP infeasible: OutsideTheRegionOfAttractionError     */
+    CARMPC_LOOP_INPUT_VIOLATION = 2,  /* check_input assertion (simulator.py:92-95)           */
+    CARMPC_LOOP_TIMEOUT = 3,          /* i >= last_step                                       */
+    CARMPC_LOOP_SOLVER_FAILURE = 4    /* QP status MAX_ITER / NUMERICAL                       */
+};
+
+typedef struct {
+    int32_t mode;          /* 0 state feedback, 1 output feedback, 2 output feedback with disturbance */
+    int32_t steps_update;  /* STEPS_UPDATE (configuration.py:13)                                       */
+    int32_t last_step;     /* loop index of the time-out: 151 (i > 30/DT), 75 (i >= 15/DT)             */
+    int32_t ny;            /* output rows (modes 1, 2), <= 8                                           */
+    double dt;             /* DT_SIMULATION                                                            */
+    double l1;             /* wheelbase (simulator.py:6-13)                                            */
+    double goal_tol;       /* 0.1 in run_MPCStateFB.py:40; <= 0 disables the goal test                 */
+    const double* goal;    /* NX host, NULL = the problem's goal                                       */
+    const double *C, *L;   /* ny*NX, NX*ny host (modes 1, 2; L = L1 in mode 2)                         */
+    const double *Cd, *L2, *Bd; /* ny, ny, NX host (mode 2)                                            */
+} carmpc_loop_desc;
+
+/* Runs the loop to completion for every instance.  Device buffers: state B*NX (in: start,
+ * out: final), xhat B*NX (modes 1, 2: in init_state, out estimate), dhat B (mode 2), xref B*NX
+ * or NULL (QP reference, NULL = goal), u B*n (out: last QP solution), outcome/steps B int32
+ * (steps = loop indices executed).  Synchronises the stream once every check_every indices to
+ * stop when no instance is left (check_every <= 0: never, run to last_step). */
+int carmpc_closed_loop_batch(const carmpc_problem* prob, int64_t batch, const carmpc_loop_desc* loop,
+                             double* state, double* xhat, double* dhat, const double* xref, double* u,
+                             int32_t* outcome, int32_t* steps, int32_t check_every,
+                             const carmpc_settings* settings, hipStream_t stream);
+
 /* Canonical per-iteration flop count of the dense condensed IPM
  * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);

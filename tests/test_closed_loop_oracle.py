@@ -1,0 +1,55 @@
+"""CPU checks of the closed-loop runner restatement (oracle/closed_loop.py) and the host
+side of carmpc_amd.closed_loop (stop indices of the example runners)."""
+import numpy as np
+
+from conftest import TERMINAL_SETS
+
+
+def _asm():
+    from oracle import assembly as oa
+    return oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+
+
+def test_runner_stop_indices():
+    from carmpc_amd.closed_loop import first_index_above, first_index_at_least
+    from carmpc_amd.configuration import DT_SIMULATION
+    # run_MPCStateFB.py:40 breaks at the first i > 30/DT; run_MPCOutputFB.py:48 at i >= 15/DT
+    assert first_index_above(30 / DT_SIMULATION) == 151
+    assert first_index_at_least(15 / DT_SIMULATION) == 75
+    assert first_index_above(2.5) == 3 and first_index_at_least(2.5) == 3
+
+
+def test_example_runs():
+    """The examples' own start states: StateFB reaches the goal box after 52 loop indices,
+    OutputFB runs to its 76-index time-out."""
+    from oracle import closed_loop as ocl
+    asm = _asm()
+    solve = ocl.c_solver(asm)
+    r = ocl.run(asm, [5, -1.5, 0.1, 0], mode=0, last_step=151, goal_tol=0.1, solve=solve)
+    assert r["outcome"] == ocl.REACHED and r["steps"] == 52
+    assert np.all(np.abs(r["state"] - asm.goal) <= 0.1)
+    r = ocl.run(asm, [5, -1.5, 0, 0], mode=1, last_step=75, goal_tol=0.0, solve=solve)
+    assert r["outcome"] == ocl.TIMEOUT and r["steps"] == 76 and len(r["trajectory"]) == 76
+
+
+def test_numpy_and_c_oracle_loops_agree():
+    from oracle import closed_loop as ocl
+    asm = _asm()
+    solve = ocl.c_solver(asm)
+    for start in ([5, -1.5, 0.1, 0], [12.0, 0.5, 0.05, 2.0], [2, -2.5, 0, 0]):
+        a = ocl.run(asm, start, mode=0, last_step=20, goal_tol=0.1)
+        b = ocl.run(asm, start, mode=0, last_step=20, goal_tol=0.1, solve=solve)
+        assert a["outcome"] == b["outcome"] and a["steps"] == b["steps"]
+        np.testing.assert_allclose(a["state"], b["state"], rtol=0, atol=1e-7)
+
+
+def test_input_violation_stops_before_the_step():
+    from oracle import closed_loop as ocl
+    asm = _asm()
+    calls = []
+
+    def bad_solver(x0, xr, d):
+        calls.append(1)
+        return 0, np.full(2 * asm.N, 3.0)     # acceleration 3 > 2.05: check_input asserts next index
+    r = ocl.run(asm, [5, -1.5, 0.1, 0], mode=0, solve=bad_solver)
+    assert r["outcome"] == ocl.INPUT_VIOLATION and r["steps"] == 1 and len(calls) == 1
