@@ -25,7 +25,7 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_observer_batch", "carmpc_plant_step_batch", "carmpc_canonical_flops_per_iter",
            "carmpc_last_error", "carmpc_version", "carmpc_problem_kernel",
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
-           "carmpc_observer_dist_batch", "carmpc_closed_loop_batch")
+           "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch")
 
 # outcomes of carmpc_closed_loop_batch (carmpc.h)
 LOOP_RUNNING, LOOP_REACHED, LOOP_INFEASIBLE, LOOP_INPUT_VIOLATION, LOOP_TIMEOUT, LOOP_SOLVER_FAILURE = -1, 0, 1, 2, 3, 4
@@ -96,6 +96,8 @@ def load():
         "carmpc_problem_set_disturbance": ([vp, dp], ctypes.c_int),
         "carmpc_solve_batch_dist": ([vp, i64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_observer_dist_batch": ([vp, i64, vp, i32, dp, dp, dp, dp, dp, vp, vp, vp, i64, vp], ctypes.c_int),
+        "carmpc_lp_batch": ([i64, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_double, vp, vp, vp, vp, vp],
+                            ctypes.c_int),
         "carmpc_closed_loop_batch": ([vp, i64, ctypes.POINTER(LoopDesc), vp, vp, vp, vp, vp, vp, vp, i32,
                                       ctypes.POINTER(Settings), vp], ctypes.c_int),
     }

@@ -718,6 +718,23 @@ int carmpc_solve_batch_dist(const carmpc_problem* P, int64_t batch, const double
     return CARMPC_OK;
 }
 
+int carmpc_lp_batch(int64_t nlp, int32_t max_m, const int64_t* a_off, const int64_t* b_off, const int32_t* m,
+                    const double* a_pool, const double* b_pool, const double* c, const int32_t* relax,
+                    double relax_amount, double* value, double* x, int32_t* status, int32_t* iters,
+                    hipStream_t stream) {
+    if (nlp < 0) return fail(CARMPC_EINVAL, "negative LP count");
+    if (nlp == 0) return CARMPC_OK;
+    if (!a_off || !b_off || !m || !a_pool || !b_pool || !c || !value || !status)
+        return fail(CARMPC_EINVAL, "null LP pointer");
+    if (max_m < 0 || max_m > 1016) return fail(CARMPC_EUNSUPPORTED, "LPs with more than 1016 rows");
+    LpArgs a{};
+    a.nlp = nlp; a.a_off = a_off; a.b_off = b_off; a.m = m; a.a_pool = a_pool; a.b_pool = b_pool; a.c = c;
+    a.relax = relax; a.relax_amount = relax_amount; a.tol = 1e-10; a.tol_gap = 1e-10; a.max_iter = 200;
+    a.value = value; a.x = x; a.status = status; a.iters = iters;
+    HIP_TRY(launch_lp(a, max_m, stream), "LP launch");
+    return CARMPC_OK;
+}
+
 int carmpc_closed_loop_batch(const carmpc_problem* P, int64_t batch, const carmpc_loop_desc* L, double* state,
                              double* xhat, double* dhat, const double* xref, double* u, int32_t* outcome,
                              int32_t* steps, int32_t check_every, const carmpc_settings* settings,

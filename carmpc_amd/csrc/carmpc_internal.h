@@ -142,6 +142,22 @@ struct LoopArgs {
 hipError_t launch_loop_init(const LoopArgs& a, hipStream_t s);
 hipError_t launch_loop_advance(const LoopArgs& a, int32_t i, hipStream_t s);
 hipError_t launch_loop_finish(const LoopArgs& a, int32_t i, hipStream_t s);
+// Batched 4-variable LPs (lp.hip): max c'x s.t. A x <= b, one per wavefront.
+struct LpArgs {
+    int64_t nlp;
+    const int64_t *a_off, *b_off;   // per LP offsets into the pools (doubles)
+    const int32_t* m;               // rows per LP
+    const double *a_pool, *b_pool;  // rows (m x 4, row-major) and right-hand sides
+    const double* c;                // nlp x 4
+    const int32_t* relax;           // per LP row index whose b is raised by relax_amount, -1 none (nullable)
+    double relax_amount;
+    double tol, tol_gap;
+    int32_t max_iter;
+    double* value;                  // nlp: max c'x (+inf unbounded)
+    double* x;                      // nlp x 4 (nullable)
+    int32_t *status, *iters;        // nlp (iters nullable)
+};
+hipError_t launch_lp(const LpArgs& a, int max_m, hipStream_t s);
 hipError_t launch_assembly(const AsmArgs& a, hipStream_t s);
 hipError_t launch_pack(const PackArgs& a, hipStream_t s);
 hipError_t launch_observer(const ObsArgs& a, hipStream_t s);

@@ -302,6 +302,57 @@ def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor
     return u, st, it
 
 
+
+LP_OPTIMAL, LP_UNBOUNDED, LP_MAX_ITER, LP_NUMERICAL = 0, 1, 2, 3
+
+
+def lp_batch(c, A_list, b_list, relax=None, relax_amount: float = 1.0, device=None, return_iters: bool = False):
+    """max c_l'x s.t. A_l x <= b_l (x in R^4) for every l on the GPU (carmpc_lp_batch).
+    ``A_list``/``b_list`` may repeat the same arrays: identical objects are uploaded once.
+    ``relax`` (per LP row index or -1) raises that row's b by ``relax_amount``.
+    Returns host arrays (value (+inf unbounded), x, status)."""
+    dev = require_gpu(device)
+    c = np.ascontiguousarray(np.asarray(c, dtype=np.float64).reshape(-1, 4))
+    L = c.shape[0]
+    if len(A_list) != L or len(b_list) != L:
+        raise ValueError("one constraint set per objective")
+    pools_a, pools_b, a_off, b_off, m = [], [], np.zeros(L, np.int64), np.zeros(L, np.int64), np.zeros(L, np.int32)
+    seen_a, seen_b = {}, {}
+    na = nb = 0
+    for l_, (A, b) in enumerate(zip(A_list, b_list)):
+        if id(A) not in seen_a:
+            Af = np.ascontiguousarray(np.asarray(A, dtype=np.float64).reshape(-1, 4))
+            seen_a[id(A)] = (na, Af.shape[0], A)
+            pools_a.append(Af.ravel())
+            na += Af.size
+        if id(b) not in seen_b:
+            bf = np.ascontiguousarray(np.asarray(b, dtype=np.float64).ravel())
+            seen_b[id(b)] = (nb, bf.size, b)
+            pools_b.append(bf)
+            nb += bf.size
+        a_off[l_], rows, _ = seen_a[id(A)]
+        b_off[l_], nrhs, _ = seen_b[id(b)]
+        if rows != nrhs:
+            raise ValueError(f"LP {l_}: {rows} rows but {nrhs} right-hand sides")
+        m[l_] = rows
+    max_m = int(m.max()) if L else 0
+    if max_m > 1016:
+        raise ValueError("LPs are limited to 1016 rows")
+    t = lambda a: torch.as_tensor(a).to(dev)  # noqa: E731
+    da, db = t(np.concatenate(pools_a) if pools_a else np.zeros(4)), t(np.concatenate(pools_b) if pools_b else np.zeros(1))
+    dao, dbo, dm, dc = t(a_off), t(b_off), t(m), t(c)
+    drel = None if relax is None else t(np.ascontiguousarray(np.asarray(relax, dtype=np.int32).ravel()))
+    val = torch.empty(L, dtype=torch.float64, device=dev)
+    x = torch.empty((L, 4), dtype=torch.float64, device=dev)
+    st = torch.empty(L, dtype=torch.int32, device=dev)
+    its = torch.empty(L, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        check(_native.load().carmpc_lp_batch(L, max_m, _tptr(dao), _tptr(dbo), _tptr(dm), _tptr(da), _tptr(db),
+                                             _tptr(dc), _tptr(drel), relax_amount, _tptr(val), _tptr(x), _tptr(st),
+                                             _tptr(its), _stream_handle(None)), "carmpc_lp_batch")
+    out = (val.cpu().numpy(), x.cpu().numpy(), st.cpu().numpy())
+    return out + (its.cpu().numpy(),) if return_iters else out
+
 def plant_step(state: torch.Tensor, u: torch.Tensor, dt: float, l1: float, stream=None) -> torch.Tensor:
     """Batched nonlinear plant (simulator.py:51-69), in place on device.  Returns the per-instance
     input-limit flags of check_input (simulator.py:83-97); flagged rows are stepped anyway."""

@@ -217,6 +217,24 @@ int carmpc_closed_loop_batch(const carmpc_problem* prob, int64_t batch, const ca
                              int32_t* outcome, int32_t* steps, int32_t check_every,
                              const carmpc_settings* settings, hipStream_t stream);
 
+/* ---- batched small LPs (terminal-set synthesis) ------------------------
+ * lib/terminal_set.py:45-67 (one LP per state row and horizon k) and the redundancy removal of
+ * the final set (polytope.reduce, called at terminal_set.py:197) as one launch:
+ *   LP l:  maximise c_l'x  s.t.  A_l x <= b_l (+ relax_amount on row relax[l]),  x in R^4
+ * A_l = a_pool[a_off[l] ...] (m[l] x 4 row-major), b_l = b_pool[b_off[l] ...] (m[l]); all
+ * DEVICE pointers; relax may be NULL.  value[l] = optimum (+inf when unbounded), x (nullable)
+ * nlp x 4, status/iters (iters nullable) nlp.  m[l] <= 1016; max_m is the largest m[l]. */
+enum {
+    CARMPC_LP_OPTIMAL = 0,
+    CARMPC_LP_UNBOUNDED = 1,
+    CARMPC_LP_MAX_ITER = 2,
+    CARMPC_LP_NUMERICAL = 3
+};
+int carmpc_lp_batch(int64_t nlp, int32_t max_m, const int64_t* a_off, const int64_t* b_off, const int32_t* m,
+                    const double* a_pool, const double* b_pool, const double* c, const int32_t* relax,
+                    double relax_amount, double* value, double* x, int32_t* status, int32_t* iters,
+                    hipStream_t stream);
+
 /* Canonical per-iteration flop count of the dense condensed IPM
  * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);
