@@ -25,7 +25,9 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_observer_batch", "carmpc_plant_step_batch", "carmpc_canonical_flops_per_iter",
            "carmpc_last_error", "carmpc_version", "carmpc_problem_kernel",
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
-           "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch")
+           "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
+           "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
+           "carmpc_hetero_get")
 
 # outcomes of carmpc_closed_loop_batch (carmpc.h)
 LOOP_RUNNING, LOOP_REACHED, LOOP_INFEASIBLE, LOOP_INPUT_VIOLATION, LOOP_TIMEOUT, LOOP_SOLVER_FAILURE = -1, 0, 1, 2, 3, 4
@@ -54,6 +56,15 @@ class LoopDesc(ctypes.Structure):
                 ("ny", ctypes.c_int32), ("dt", ctypes.c_double), ("l1", ctypes.c_double),
                 ("goal_tol", ctypes.c_double), ("goal", _dp), ("C", _dp), ("L", _dp), ("Cd", _dp), ("L2", _dp),
                 ("Bd", _dp)]
+
+
+class HeteroDesc(ctypes.Structure):
+    """carmpc_hetero_desc (include/carmpc.h)."""
+    _dp = ctypes.POINTER(ctypes.c_double)
+    _fields_ = [("N", ctypes.c_int32), ("dt", ctypes.c_double), ("l1", ctypes.c_double), ("Q", _dp), ("R", _dp),
+                ("n_state_rows", ctypes.c_int32), ("state_A", _dp), ("state_b", _dp),
+                ("n_term_rows", ctypes.c_int32), ("term_A", _dp), ("term_b", _dp),
+                ("u_lower", _dp), ("u_upper", _dp), ("goal", _dp)]
 
 
 class Settings(ctypes.Structure):
@@ -98,6 +109,11 @@ def load():
         "carmpc_observer_dist_batch": ([vp, i64, vp, i32, dp, dp, dp, dp, dp, vp, vp, vp, i64, vp], ctypes.c_int),
         "carmpc_lp_batch": ([i64, i32, vp, vp, vp, vp, vp, vp, vp, ctypes.c_double, vp, vp, vp, vp, vp],
                             ctypes.c_int),
+        "carmpc_hetero_create": ([ctypes.POINTER(HeteroDesc), i64, ctypes.POINTER(vp)], ctypes.c_int),
+        "carmpc_hetero_destroy": ([vp], None),
+        "carmpc_hetero_linearize": ([vp, vp, vp, vp], ctypes.c_int),
+        "carmpc_hetero_solve": ([vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
+        "carmpc_hetero_get": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "carmpc_closed_loop_batch": ([vp, i64, ctypes.POINTER(LoopDesc), vp, vp, vp, vp, vp, vp, vp, i32,
                                       ctypes.POINTER(Settings), vp], ctypes.c_int),
     }

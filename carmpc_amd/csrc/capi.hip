@@ -50,6 +50,40 @@ struct carmpc_problem {
     }
 };
 
+struct carmpc_hetero {
+    DevProblem dev{};     // shared part (n, nv, ldg, boxed, N, nu, lb, ub, goal) + slice bases
+    int64_t batch = 0;
+    int p_all = 0, nt = 0, ns = 0;
+    double dt = 0.0, l1 = 0.0;
+    int device = 0;
+    bool ready = false;   // carmpc_hetero_linearize ran
+    std::vector<void*> allocs;
+    double *Q = nullptr, *R = nullptr, *tA = nullptr, *tb = nullptr, *sA = nullptr, *sb = nullptr;
+    double *A = nullptr, *B = nullptr, *P = nullptr, *K = nullptr;
+    int32_t* lin_status = nullptr;
+    double *G = nullptr, *H = nullptr, *hq = nullptr, *w0 = nullptr, *E = nullptr, *pw = nullptr, *pE = nullptr;
+    int32_t *partner = nullptr, *p = nullptr, *npre = nullptr;
+    ~carmpc_hetero() {
+        for (void* q : allocs) (void)hipFree(q);
+    }
+    template <class T_>
+    hipError_t alloc(T_** ptr, size_t count) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T_));
+        if (e == hipSuccess) {
+            allocs.push_back(q);
+            *ptr = static_cast<T_*>(q);
+        }
+        return e;
+    }
+    template <class T_>
+    hipError_t upload(T_** ptr, const T_* src, size_t count) {
+        hipError_t e = alloc(ptr, count);
+        if (e == hipSuccess && count) e = hipMemcpy(*ptr, src, count * sizeof(T_), hipMemcpyHostToDevice);
+        return e;
+    }
+};
+
 namespace {
 thread_local std::string g_err;
 
@@ -715,6 +749,129 @@ int carmpc_solve_batch_dist(const carmpc_problem* P, int64_t batch, const double
     hipError_t e = launch_solve(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
     if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
     if (e != hipSuccess) return hipfail(e, "solve launch");
+    return CARMPC_OK;
+}
+
+int carmpc_hetero_create(const carmpc_hetero_desc* d, int64_t batch, carmpc_hetero** out) {
+    if (!d || !out) return fail(CARMPC_EINVAL, "null argument");
+    *out = nullptr;
+    if (batch < 1) return fail(CARMPC_EINVAL, "batch must be >= 1");
+    if (d->N < 1 || d->N > 32) return fail(CARMPC_EUNSUPPORTED, "N must be in [1,32]");
+    if (!d->Q || !d->R || !d->goal) return fail(CARMPC_EINVAL, "null model matrix");
+    if (!(d->dt > 0.0) || !(d->l1 > 0.0)) return fail(CARMPC_EINVAL, "dt and l1 must be positive");
+    if (d->n_state_rows < 0 || d->n_term_rows < 0) return fail(CARMPC_EINVAL, "negative row count");
+    if ((d->n_state_rows && (!d->state_A || !d->state_b)) || (d->n_term_rows && (!d->term_A || !d->term_b)))
+        return fail(CARMPC_EINVAL, "null constraint rows");
+    if ((d->u_lower == nullptr) != (d->u_upper == nullptr)) return fail(CARMPC_EINVAL, "u_lower/u_upper mismatch");
+    const int N = d->N, n = 2 * N;
+    const int nv = dense_pick_nv(n);
+    const int p_all = d->n_term_rows + d->n_state_rows * N;
+    if (nv < 0) return fail(CARMPC_EUNSUPPORTED, "2N must be <= 64");
+    if (p_all > 256 || p_all > kHetMaxRows)
+        return fail(CARMPC_EUNSUPPORTED, "per-instance problems are limited to 256 general rows (p_all=" +
+                                             std::to_string(p_all) + ")");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto* h = new carmpc_hetero();
+    h->device = dev;
+    h->batch = batch; h->p_all = p_all; h->nt = d->n_term_rows; h->ns = d->n_state_rows; h->dt = d->dt; h->l1 = d->l1;
+    DevProblem& D = h->dev;
+    D.n = n; D.nv = nv; D.ldg = nv + 2; D.N = N; D.nu = 2; D.p = p_all;
+    std::vector<double> lbp(nv, -1.0), ubp(nv, 1.0);
+    if (d->u_lower)
+        for (int k = 0; k < N; ++k)
+            for (int c = 0; c < 2; ++c) { lbp[k * 2 + c] = d->u_lower[c]; ubp[k * 2 + c] = d->u_upper[c]; }
+    D.boxed = d->u_lower ? 1 : 0;
+    const int64_t sG = (int64_t)std::max(p_all, 1) * D.ldg, sH = (int64_t)nv * nv, sHq = (int64_t)nv * NX,
+                  sRow = std::max(p_all, 1);
+    double *dlb, *dub, *dgoal;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+    chk(h->upload(&dlb, lbp.data(), lbp.size()));
+    chk(h->upload(&dub, ubp.data(), ubp.size()));
+    chk(h->upload(&dgoal, d->goal, NX));
+    chk(h->upload(&h->Q, d->Q, 16));
+    chk(h->upload(&h->R, d->R, 4));
+    chk(h->upload(&h->tA, d->term_A, (size_t)h->nt * NX));
+    chk(h->upload(&h->tb, d->term_b, (size_t)h->nt));
+    chk(h->upload(&h->sA, d->state_A, (size_t)h->ns * NX));
+    chk(h->upload(&h->sb, d->state_b, (size_t)h->ns));
+    chk(h->alloc(&h->A, (size_t)batch * 16)); chk(h->alloc(&h->B, (size_t)batch * 8));
+    chk(h->alloc(&h->P, (size_t)batch * 16)); chk(h->alloc(&h->K, (size_t)batch * 8));
+    chk(h->alloc(&h->lin_status, (size_t)batch));
+    chk(h->alloc(&h->G, (size_t)batch * sG)); chk(h->alloc(&h->H, (size_t)batch * sH));
+    chk(h->alloc(&h->hq, (size_t)batch * sHq)); chk(h->alloc(&h->w0, (size_t)batch * sRow));
+    chk(h->alloc(&h->E, (size_t)batch * sRow * NX)); chk(h->alloc(&h->pw, (size_t)batch * sRow));
+    chk(h->alloc(&h->pE, (size_t)batch * sRow * NX)); chk(h->alloc(&h->partner, (size_t)batch * sRow));
+    chk(h->alloc(&h->p, (size_t)batch)); chk(h->alloc(&h->npre, (size_t)batch));
+    if (e != hipSuccess) {
+        delete h;
+        return hipfail(e, "hetero allocation (per-instance problem slices)");
+    }
+    D.lb = dlb; D.ub = dub; D.goal = dgoal;
+    D.G = h->G; D.H = h->H; D.hq = h->hq; D.w0 = h->w0; D.E = h->E; D.pre_w0 = h->pw; D.pre_E = h->pE;
+    D.partner = h->partner; D.het_p = h->p; D.het_npre = h->npre;
+    D.het_sG = sG; D.het_sH = sH; D.het_sHq = sHq; D.het_sRow = sRow;
+    *out = h;
+    return CARMPC_OK;
+}
+
+void carmpc_hetero_destroy(carmpc_hetero* h) { delete h; }
+
+int carmpc_hetero_linearize(carmpc_hetero* h, const double* lin_state, const double* lin_input, hipStream_t stream) {
+    if (!h || !lin_state || !lin_input) return fail(CARMPC_EINVAL, "null argument");
+    LinArgs l{};
+    l.batch = h->batch; l.dt = h->dt; l.l1 = h->l1; l.lin_state = lin_state; l.lin_input = lin_input;
+    l.Q = h->Q; l.R = h->R; l.A = h->A; l.B = h->B; l.P = h->P; l.K = h->K; l.status = h->lin_status;
+    HIP_TRY(launch_linearize(l, stream), "linearize launch");
+    HetAsmArgs a{};
+    a.batch = h->batch; a.N = h->dev.N; a.nv = h->dev.nv; a.ldg = h->dev.ldg; a.nt = h->nt; a.ns = h->ns;
+    a.A = h->A; a.B = h->B; a.P = h->P; a.Q = h->Q; a.R = h->R;
+    a.term_A = h->tA; a.term_b = h->tb; a.state_A = h->sA; a.state_b = h->sb;
+    a.G = h->G; a.H = h->H; a.hq = h->hq; a.w0 = h->w0; a.E = h->E; a.pre_w0 = h->pw; a.pre_E = h->pE;
+    a.partner = h->partner; a.p = h->p; a.npre = h->npre;
+    a.strideG = h->dev.het_sG; a.strideH = h->dev.het_sH; a.strideHq = h->dev.het_sHq; a.strideRow = h->dev.het_sRow;
+    HIP_TRY(launch_hetero_assembly(a, stream), "hetero assembly launch");
+    h->ready = true;
+    return CARMPC_OK;
+}
+
+int carmpc_hetero_solve(const carmpc_hetero* h, const double* x0, const double* xref, double* u_out, int32_t* status,
+                        int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
+    if (!h) return fail(CARMPC_EINVAL, "null handle");
+    if (!h->ready) return fail(CARMPC_EINVAL, "call carmpc_hetero_linearize first");
+    if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
+    const Settings s = make_settings(settings);
+    int unsupported = 0;
+    hipError_t e = launch_dense_het(h->dev, h->p_all, h->batch, x0, xref, u_out, h->dev.n, status, iters, s, stream,
+                                    &unsupported);
+    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+    if (e != hipSuccess) return hipfail(e, "hetero solve launch");
+    return CARMPC_OK;
+}
+
+int carmpc_hetero_get(const carmpc_hetero* h, double* A, double* B, double* P, double* K, int32_t* dare_status,
+                      int32_t* p, int32_t* npre, double* G, double* H, double* hq, double* w0, double* E,
+                      int64_t* dims) {
+    if (!h) return fail(CARMPC_EINVAL, "null handle");
+    const size_t b = (size_t)h->batch;
+    const DevProblem& D = h->dev;
+    if (dims) {
+        dims[0] = D.het_sRow; dims[1] = D.ldg; dims[2] = D.nv; dims[3] = D.n; dims[4] = h->p_all; dims[5] = h->batch;
+    }
+    if (!h->ready && (A || B || P || K || dare_status || p || npre || G || H || hq || w0 || E))
+        return fail(CARMPC_EINVAL, "call carmpc_hetero_linearize first");
+    struct Item { void* dst; const void* src; size_t bytes; } items[] = {
+        {A, h->A, sizeof(double) * b * 16},          {B, h->B, sizeof(double) * b * 8},
+        {P, h->P, sizeof(double) * b * 16},          {K, h->K, sizeof(double) * b * 8},
+        {dare_status, h->lin_status, sizeof(int32_t) * b},
+        {p, h->p, sizeof(int32_t) * b},              {npre, h->npre, sizeof(int32_t) * b},
+        {G, h->G, sizeof(double) * b * D.het_sG},    {H, h->H, sizeof(double) * b * D.het_sH},
+        {hq, h->hq, sizeof(double) * b * D.het_sHq}, {w0, h->w0, sizeof(double) * b * D.het_sRow},
+        {E, h->E, sizeof(double) * b * D.het_sRow * NX}};
+    HIP_TRY(hipDeviceSynchronize(), "hetero_get sync");
+    for (auto& it : items)
+        if (it.dst) HIP_TRY(hipMemcpy(it.dst, it.src, it.bytes, hipMemcpyDeviceToHost), "hetero_get");
     return CARMPC_OK;
 }
 

@@ -80,6 +80,11 @@ struct DevProblem {
     const double* pre_Ed;     // npre
     const double* s_Ed;       // srs*64 (staged slots)
     const double* r_Ed;       // 256 (Riccati slots)
+    // per-instance problems (hetero.hip, ipm_dense.hip HET): G, H, w0, E, hq, pre_w0, pre_E,
+    // partner above are the bases of per-instance slices; p / npre per instance
+    const int32_t* het_p;     // batch (nullptr: shared problem)
+    const int32_t* het_npre;  // batch
+    int64_t het_sG, het_sH, het_sHq, het_sRow;   // slice strides in elements
 };
 
 struct Settings {
@@ -158,6 +163,32 @@ struct LpArgs {
     int32_t *status, *iters;        // nlp (iters nullable)
 };
 hipError_t launch_lp(const LpArgs& a, int max_m, hipStream_t s);
+// Per-instance linearisation / DARE / assembly (hetero.hip).
+constexpr int kHetMaxRows = 1024;
+constexpr int kDareMaxIter = 60;
+struct LinArgs {
+    int64_t batch;
+    double dt, l1;
+    const double *lin_state, *lin_input;   // B x 4, B x 2
+    const double *Q, *R;                   // 16, 4 (device)
+    double *A, *B, *P, *K;                 // B x 16, B x 8, B x 16, B x 8 (K nullable)
+    int32_t* status;                       // B: doubling steps, -1 = no stabilising solution (P = 0)
+};
+struct HetAsmArgs {
+    int64_t batch;
+    int N, nv, ldg, nt, ns;
+    const double *A, *B, *P;               // per instance, from LinArgs
+    const double *Q, *R;
+    const double *term_A, *term_b, *state_A, *state_b;
+    double *G, *H, *hq, *w0, *E, *pre_w0, *pre_E;
+    int32_t *partner, *p, *npre;
+    int64_t strideG, strideH, strideHq, strideRow;
+};
+hipError_t launch_linearize(const LinArgs& a, hipStream_t s);
+hipError_t launch_hetero_assembly(const HetAsmArgs& a, hipStream_t s);
+hipError_t launch_dense_het(const DevProblem& P, int p_max, int64_t batch, const double* x0, const double* xref,
+                            double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s,
+                            hipStream_t stream, int* unsupported);
 hipError_t launch_assembly(const AsmArgs& a, hipStream_t s);
 hipError_t launch_pack(const PackArgs& a, hipStream_t s);
 hipError_t launch_observer(const ObsArgs& a, hipStream_t s);

@@ -190,7 +190,9 @@ __device__ __forceinline__ double chol_solve(const double (&M)[NV], double inv_i
 
 }  // namespace
 
-template <int NV, int RS, int kWPB>
+// HET: every instance has its own problem slice (hetero.hip; G, H read from global memory,
+// p / npre per instance); otherwise one problem per launch with G, H in LDS.
+template <int NV, int RS, int kWPB, bool HET = false>
 __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int64_t batch,
                                                               const double* __restrict__ x0,
                                                               const double* __restrict__ xref,
@@ -202,13 +204,15 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int p = P.p;
+    int p = P.p;
     const int ldg = P.ldg;
     double* Gs = smem;
     double* Hs = Gs + ((p * ldg + 1) & ~1);
-    for (int i = threadIdx.x; i < p * ldg; i += blockDim.x) Gs[i] = P.G[i];
-    for (int i = threadIdx.x; i < NV * NV; i += blockDim.x) Hs[i] = P.H[i];
-    __syncthreads();
+    if (!HET) {
+        for (int i = threadIdx.x; i < p * ldg; i += blockDim.x) Gs[i] = P.G[i];
+        for (int i = threadIdx.x; i < NV * NV; i += blockDim.x) Hs[i] = P.H[i];
+        __syncthreads();
+    }
 
     WaveCtx<NV, RS> W;
     W.Gs = Gs; W.Hs = Hs; W.bvec = wscr[wave]; W.rvec = wscr[wave] + 64;
@@ -220,13 +224,34 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
     const double lb = boxact ? P.lb[W.li] : -UNBOXED_BOUND;
     const double ub = boxact ? P.ub[W.li] : UNBOXED_BOUND;
     const double bndabs = fmax(fabs(lb), fabs(ub));
-    const int m_rows = p + (P.boxed ? 2 * NV : 0);
-    const double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
+    int m_rows = p + (P.boxed ? 2 * NV : 0);
+    double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
 
     // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
     const int64_t nlive = S.count ? (int64_t)*S.count : batch;
     for (int64_t slot = (int64_t)blockIdx.x * kWPB + wave; slot < nlive; slot += (int64_t)gridDim.x * kWPB) {
         const int64_t inst = S.index ? (int64_t)S.index[slot] : slot;
+        // this instance's rows (shared problem: the launch's; HET: its own slice)
+        const double *Pw0 = P.w0, *PE = P.E, *Phq = P.hq, *Ppw = P.pre_w0, *PpE = P.pre_E;
+        const int32_t* Ppart = P.partner;
+        int npre = P.npre;
+        if (HET) {
+            p = P.het_p[inst];
+            npre = P.het_npre[inst];
+            W.Gs = P.G + inst * P.het_sG;
+            W.Hs = P.H + inst * P.het_sH;
+            W.p = p;
+#pragma unroll
+            for (int s = 0; s < RS; ++s) W.rv[s] = (s * 64 + lane) < p;
+            m_rows = p + (P.boxed ? 2 * NV : 0);
+            inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
+            Pw0 += inst * P.het_sRow;
+            PE += inst * P.het_sRow * NX;
+            Ppw += inst * P.het_sRow;
+            PpE += inst * P.het_sRow * NX;
+            Ppart += inst * P.het_sRow;
+            Phq += inst * P.het_sHq;
+        }
         double xv[NX], xr[NX];
 #pragma unroll
         for (int k = 0; k < NX; ++k) {
@@ -236,10 +261,10 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
         // ---- x0-only rows (G_r == 0): preconditions on x0 ---------------------
         const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
         bool bad = false;
-        for (int r = lane; r < P.npre; r += 64) {
-            double v = P.pre_w0[r];
+        for (int r = lane; r < npre; r += 64) {
+            double v = Ppw[r];
 #pragma unroll
-            for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv[k];
+            for (int k = 0; k < NX; ++k) v -= PpE[r * NX + k] * xv[k];
             if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
             bad |= v < -PRE_TOL;
         }
@@ -255,7 +280,7 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
         double q = 0.0;
         if (act) {
 #pragma unroll
-            for (int k = 0; k < NX; ++k) q += P.hq[W.li * NX + k] * (xv[k] - xr[k]);
+            for (int k = 0; k < NX; ++k) q += Phq[W.li * NX + k] * (xv[k] - xr[k]);
         }
         double w[RS];
 #pragma unroll
@@ -263,9 +288,9 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
             const int r = s * 64 + lane;
             double v = 0.0;
             if (W.rv[s]) {
-                v = P.w0[r];
+                v = Pw0[r];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v -= P.E[r * NX + k] * xv[k];
+                for (int k = 0; k < NX; ++k) v -= PE[r * NX + k] * xv[k];
                 if (P.Ed) v -= P.Ed[r] * dd;
             }
             w[s] = v;
@@ -465,14 +490,14 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
                 bool paired[RS];
 #pragma unroll
                 for (int s = 0; s < RS; ++s) paired[s] = false;
-                if (P.partner) {
+                if (Ppart) {
                     __builtin_amdgcn_wave_barrier();
 #pragma unroll
                     for (int s = 0; s < RS; ++s) W.rvec[s * 64 + lane] = (W.rv[s] && dg[s] != 0.0) ? ra[s] : NAN;
                     __builtin_amdgcn_wave_barrier();
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
-                        const int pr = W.rv[s] ? P.partner[s * 64 + lane] : -1;
+                        const int pr = W.rv[s] ? Ppart[s * 64 + lane] : -1;
                         paired[s] = pr >= 0 && dg[s] != 0.0 && !isnan(W.rvec[pr]);
                     }
                 }
@@ -581,7 +606,65 @@ hipError_t launch_rs(int rs, const DevProblem& P, int64_t batch, const double* x
         default: return hipErrorInvalidValue;
     }
 }
+template <int NV, int RS>
+hipError_t launch_het_t(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
+                        int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
+    constexpr int kWPB = 4;
+    auto kern = ipm_dense_kernel<NV, RS, kWPB, true>;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kWPB * 64, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    int64_t want = (batch + kWPB - 1) / kWPB;
+    int64_t grid = (int64_t)cus * per_cu;
+    if (want < grid) grid = want;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
+                       status, iters, s);
+    return hipGetLastError();
+}
+template <int NV>
+hipError_t launch_het_rs(int rs, const DevProblem& P, int64_t batch, const double* x0, const double* xref,
+                         double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s,
+                         hipStream_t stream) {
+    switch (rs) {
+        case 1: return launch_het_t<NV, 1>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 2: return launch_het_t<NV, 2>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 3: return launch_het_t<NV, 3>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 4: return launch_het_t<NV, 4>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
 }  // namespace
+
+hipError_t launch_dense_het(const DevProblem& P, int p_max, int64_t batch, const double* x0, const double* xref,
+                            double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s,
+                            hipStream_t stream, int* unsupported) {
+    *unsupported = 0;
+    if (batch <= 0) return hipSuccess;
+    int rs = (p_max + 63) / 64;
+    if (rs < 1) rs = 1;
+    if (rs > kMaxRS) {
+        *unsupported = 1;
+        return hipErrorInvalidValue;
+    }
+    switch (P.nv) {
+        case 8: return launch_het_rs<8>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 16: return launch_het_rs<16>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 20: return launch_het_rs<20>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 24: return launch_het_rs<24>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 32: return launch_het_rs<32>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 40: return launch_het_rs<40>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 48: return launch_het_rs<48>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        case 64: return launch_het_rs<64>(rs, P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
+        default: *unsupported = 1; return hipErrorInvalidValue;
+    }
+}
+
 
 int dense_pick_nv(int n) {
     for (int nv : kNVs)

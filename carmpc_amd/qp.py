@@ -303,6 +303,89 @@ def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor
 
 
 
+
+class HeteroQP:
+    """Per-instance linear-MPC QPs (carmpc_hetero_*): instance b is linearised at its own
+    (lin_state[b], lin_input[b]); A, B, the DARE terminal cost P, K and the condensed QP are
+    built on the device.  Constraint rows, Q, R, box and goal are shared."""
+
+    def __init__(self, *, N: int, batch: int, dt: float, l1: float, Q, R, goal, state_A=None, state_b=None,
+                 term_A=None, term_b=None, u_lower=None, u_upper=None, device=None):
+        self.device = require_gpu(device)
+        lib = _native.load()
+        Q, R, goal = _f64(Q), _f64(R), _f64(goal)
+        sA = _f64(state_A if state_A is not None else np.zeros((0, NX)))
+        sb = _f64(state_b if state_b is not None else np.zeros(0))
+        tA = _f64(term_A if term_A is not None else np.zeros((0, NX)))
+        tb = _f64(term_b if term_b is not None else np.zeros(0))
+        lo, hi = _f64(u_lower), _f64(u_upper)
+        self._keep = (Q, R, goal, sA, sb, tA, tb, lo, hi)
+        d = _native.HeteroDesc(N=N, dt=dt, l1=l1, Q=_dptr(Q), R=_dptr(R), n_state_rows=sA.shape[0],
+                               state_A=_dptr(sA), state_b=_dptr(sb), n_term_rows=tA.shape[0], term_A=_dptr(tA),
+                               term_b=_dptr(tb), u_lower=_dptr(lo), u_upper=_dptr(hi), goal=_dptr(goal))
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.carmpc_hetero_create(ctypes.byref(d), int(batch), ctypes.byref(handle)), "carmpc_hetero_create")
+        self._h = handle
+        self.N, self.batch, self.n = N, int(batch), 2 * N
+        self.goal = goal.copy()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _native.load().carmpc_hetero_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def linearize(self, lin_state, lin_input, stream=None) -> None:
+        """(Re)build every instance's model and QP at its linearisation point (device, stream-ordered)."""
+        ls = _as_dev(lin_state, self.device)
+        li = _as_dev(lin_input, self.device, width=2)
+        if ls.shape[0] != self.batch or li.shape[0] != self.batch:
+            raise ValueError(f"expected {self.batch} linearisation points")
+        self._lin = (ls, li)   # kernels read them asynchronously
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_hetero_linearize(self._h, _tptr(ls), _tptr(li), _stream_handle(stream)),
+                  "carmpc_hetero_linearize")
+
+    def solve(self, x0, xref=None, settings: SolverSettings | None = None, stream=None):
+        """(u (B x 2N), status, iters) on device for x0 (B x 4); xref defaults to the goal."""
+        x0 = _as_dev(x0, self.device)
+        if x0.shape[0] != self.batch:
+            raise ValueError(f"x0 must have {self.batch} rows")
+        if xref is not None:
+            xref = _as_dev(xref, self.device)
+            if xref.shape[0] == 1 and self.batch > 1:
+                xref = xref.expand(self.batch, NX).contiguous()
+        u = torch.empty((self.batch, self.n), dtype=torch.float64, device=self.device)
+        st = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        it = torch.empty(self.batch, dtype=torch.int32, device=self.device)
+        s = (settings or SolverSettings()).c()
+        with torch.cuda.device(self.device):
+            check(_native.load().carmpc_hetero_solve(self._h, _tptr(x0), _tptr(xref), _tptr(u), _tptr(st), _tptr(it),
+                                                     ctypes.byref(s), _stream_handle(stream)), "carmpc_hetero_solve")
+        return u, st, it
+
+    def get(self) -> dict:
+        """Per-instance model and QP slices as host numpy (carmpc_hetero_get): A, B, P, K,
+        dare_status, p, npre, G (B x R x ldg), H (B x nv x nv), hq (B x nv x 4), w0, E."""
+        lib = _native.load()
+        dims = (ctypes.c_int64 * 6)()
+        check(lib.carmpc_hetero_get(self._h, *([None] * 12), dims), "carmpc_hetero_get")
+        R, ldg, nv, _n, _pa, B = (int(v) for v in dims)
+        out = dict(A=np.empty((B, 4, 4)), B=np.empty((B, 4, 2)), P=np.empty((B, 4, 4)), K=np.empty((B, 2, 4)),
+                   dare_status=np.empty(B, np.int32), p=np.empty(B, np.int32), npre=np.empty(B, np.int32),
+                   G=np.empty((B, R, ldg)), H=np.empty((B, nv, nv)), hq=np.empty((B, nv, NX)), w0=np.empty((B, R)),
+                   E=np.empty((B, R, NX)))
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        with torch.cuda.device(self.device):
+            check(lib.carmpc_hetero_get(self._h, *[ptr(out[k]) for k in ("A", "B", "P", "K", "dare_status", "p", "npre",
+                                                                          "G", "H", "hq", "w0", "E")], dims),
+                  "carmpc_hetero_get")
+        return out
+
 LP_OPTIMAL, LP_UNBOUNDED, LP_MAX_ITER, LP_NUMERICAL = 0, 1, 2, 3
 
 

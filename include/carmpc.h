@@ -235,6 +235,42 @@ int carmpc_lp_batch(int64_t nlp, int32_t max_m, const int64_t* a_off, const int6
                     double relax_amount, double* value, double* x, int32_t* status, int32_t* iters,
                     hipStream_t stream);
 
+/* ---- per-instance linearisation -------------------------------------
+ * Every instance b has its own linearisation point (lin_state[b], lin_input[b]): A, B
+ * (mpc.py:128-180), P = DARE (mpc.py:67-74; zeros when no stabilising solution), K (mpc.py:80-81)
+ * and the condensed QP (matrix_gen.py:6-72, mpc.py:196-253) are built on the device, one slice per
+ * instance, and solved by the dense kernel reading each instance's slice.  Rows, Q, R, box and goal
+ * are shared (they do not depend on the linearisation point). */
+typedef struct carmpc_hetero carmpc_hetero;
+typedef struct {
+    int32_t N;             /* horizon, 2N <= 64                                   */
+    double dt, l1;         /* DT_CONTROL, wheelbase (simulator.py:6)              */
+    const double *Q, *R;   /* 4x4, 2x2 host                                       */
+    int32_t n_state_rows;  /* per-step rows on x_1..x_N (mpc.py:222-253)          */
+    const double *state_A, *state_b;
+    int32_t n_term_rows;   /* terminal rows on x_N (mpc.py:96-117)                 */
+    const double *term_A, *term_b;
+    const double *u_lower, *u_upper; /* nu = 2 host, NULL = no input box       */
+    const double* goal;    /* NX host, default reference                          */
+} carmpc_hetero_desc;
+/* Allocates per-instance slices for `batch` instances (n_term + N n_state <= 256 rows). */
+int carmpc_hetero_create(const carmpc_hetero_desc* desc, int64_t batch, carmpc_hetero** out);
+void carmpc_hetero_destroy(carmpc_hetero* h);
+/* (Re)linearise every instance at lin_state (B x 4) / lin_input (B x 2), DEVICE pointers, and
+ * assemble its QP; stream-ordered, no host synchronisation (successive linearisation loops). */
+int carmpc_hetero_linearize(carmpc_hetero* h, const double* lin_state, const double* lin_input,
+                            hipStream_t stream);
+/* carmpc_solve_batch semantics over the handle's instances (x0, xref B x 4, u_out B x 2N). */
+int carmpc_hetero_solve(const carmpc_hetero* h, const double* x0, const double* xref, double* u_out,
+                        int32_t* status, int32_t* iters, const carmpc_settings* settings, hipStream_t stream);
+/* Copy the per-instance model and QP slices to HOST buffers (any pointer may be NULL; synchronous):
+ * A B x 16, B B x 8, P B x 16, K B x 8, dare_status B (doubling steps, -1 = no stabilising solution,
+ * P = 0), p / npre B (QP rows / x0-only rows), G B x R x ldg (unit rows), H B x nv x nv,
+ * hq B x nv x 4, w0 B x R, E B x R x 4 with dims = {R, ldg, nv, n, rows before the split, B}. */
+int carmpc_hetero_get(const carmpc_hetero* h, double* A, double* B, double* P, double* K, int32_t* dare_status,
+                      int32_t* p, int32_t* npre, double* G, double* H, double* hq, double* w0, double* E,
+                      int64_t* dims);
+
 /* Canonical per-iteration flop count of the dense condensed IPM
  * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);

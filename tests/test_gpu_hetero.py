@@ -1,0 +1,140 @@
+"""GPU parity of per-instance linearisation (carmpc_hetero_*).
+
+Against oracle/assembly.py::build at each instance's linearisation point (which restates
+mpc.py:22-117 and matrix_gen.py:6-72, with scipy's DARE as the reference calls it):
+A, B exact to 1e-15, P and K to 1e-9 relative, the condensed QP slices to 1e-9, and the
+solutions to 1e-6 of the KKT-certified optimum (oracle/qp.py::solve_instance) with the
+same optimal / infeasible status."""
+import numpy as np
+import pytest
+
+from conftest import TERMINAL_SETS
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-6
+
+
+def _lin_points(B, seed):
+    rng = np.random.default_rng(seed)
+    ls = np.column_stack([rng.uniform(0, 30, B), rng.uniform(-2, 2, B), rng.uniform(-0.35, 0.35, B),
+                          rng.uniform(0.5, 5.0, B)])
+    li = np.column_stack([rng.uniform(-1, 1, B), rng.uniform(-0.3, 0.3, B)])
+    ls[0], li[0] = [0, 0, 0, 3], [0, 0]     # the reference's own point (configuration.py:12-13)
+    return ls, li
+
+
+def _fleet(B, seed, env="RoadMultipleCarsEnv", N=20):
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.hetero import MPCStateFBBatch
+    ls, li = _lin_points(B, seed)
+    fleet = MPCStateFBBatch(0.2, N, ls, li, env=ENVIRONMENTS[env](), terminal_set_dir=TERMINAL_SETS)
+    return fleet, ls, li
+
+
+def test_linearize_kernel_vs_reference_model(gpu_available):
+    from oracle import assembly as oa
+    fleet, ls, li = _fleet(96, 1)
+    m = fleet.model()
+    for b in range(len(ls)):
+        asm = oa.build("RoadMultipleCarsEnv", 20, lin_state=ls[b], lin_input=li[b], terminal_set_dir=TERMINAL_SETS)
+        np.testing.assert_allclose(m["A"][b], asm.A, rtol=0, atol=1e-15)
+        np.testing.assert_allclose(m["B"][b], asm.B, rtol=0, atol=1e-15)
+        np.testing.assert_allclose(m["P"][b], asm.P, rtol=1e-9, atol=1e-9 * np.abs(asm.P).max())
+        np.testing.assert_allclose(m["K"][b], asm.K, rtol=1e-9, atol=1e-9 * np.abs(asm.K).max())
+        assert m["dare_status"][b] > 0
+
+
+def test_dare_without_stabilising_solution(gpu_available):
+    """v = 0: the heading is uncontrollable, scipy raises and the reference falls back to P = 0
+    (mpc.py:69-74); the device DARE reports it and returns P = 0 too."""
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.hetero import MPCStateFBBatch
+    ls = np.array([[0, 0, 0, 0.0], [0, 0, 0, 3.0]])
+    li = np.zeros((2, 2))
+    fleet = MPCStateFBBatch(0.2, 20, ls, li, env=ENVIRONMENTS["RoadMultipleCarsEnv"](), terminal_set_dir=TERMINAL_SETS)
+    m = fleet.model()
+    assert m["dare_status"][0] == -1 and np.all(m["P"][0] == 0.0) and np.all(m["K"][0] == 0.0)
+    assert m["dare_status"][1] > 0
+
+
+def test_per_instance_qp_slices(gpu_available):
+    from oracle import assembly as oa
+    from oracle import qp as oq
+    fleet, ls, li = _fleet(24, 2)
+    g = fleet.qp.get()
+    n = 40
+    for b in range(len(ls)):
+        asm = oa.build("RoadMultipleCarsEnv", 20, lin_state=ls[b], lin_input=li[b], terminal_set_dir=TERMINAL_SETS)
+        Gn, w0n, En, keep, pre_w0, pre_E = oq.normalize_rows(asm.G, asm.w0, asm.E)
+        p = len(w0n)
+        assert g["p"][b] == p and g["npre"][b] == len(pre_w0)
+        sc = np.abs(asm.H).max()
+        np.testing.assert_allclose(g["H"][b][:n, :n], asm.H, rtol=0, atol=1e-9 * sc)
+        np.testing.assert_allclose(g["hq"][b][:n], asm.h, rtol=0, atol=1e-9 * np.abs(asm.h).max())
+        np.testing.assert_allclose(g["G"][b][:p, :n], Gn, rtol=0, atol=1e-9)
+        np.testing.assert_allclose(g["w0"][b][:p], w0n, rtol=0, atol=1e-9 * (1 + np.abs(w0n).max()))
+        np.testing.assert_allclose(g["E"][b][:p], En, rtol=0, atol=1e-9 * (1 + np.abs(En).max()))
+
+
+@pytest.mark.parametrize("env", ["RoadEnv", "RoadOneCarEnv", "RoadMultipleCarsEnv"])
+def test_per_instance_solve_vs_oracle(gpu_available, env):
+    import torch
+    from oracle import assembly as oa
+    from oracle import qp as oq
+    B = 48
+    fleet, ls, li = _fleet(B, 3, env=env)
+    rng = np.random.default_rng(7)
+    goal = fleet.goal
+    x0 = np.column_stack([rng.uniform(0, 28, B), rng.uniform(-2.5, 2.5, B), rng.uniform(-0.3, 0.3, B),
+                          rng.uniform(0, 4, B)])
+    x0[:B // 4] = goal + rng.normal(scale=0.3, size=(B // 4, 4))
+    _u0, u, st = fleet.step_batch(torch.as_tensor(x0).cuda())
+    u, st = u.cpu().numpy(), st.cpu().numpy()
+    statuses = set()
+    for b in range(B):
+        asm = oa.build(env, 20, lin_state=ls[b], lin_input=li[b], terminal_set_dir=TERMINAL_SETS)
+        r = oq.solve_instance(asm, x0[b])
+        statuses.add(r["status"])
+        if r["status"] == 0 and r["certified"]:
+            assert st[b] == 0, b
+            assert np.abs(u[b] - r["u_exact"]).max() <= U_TOL, b
+        elif r["status"] == 1:
+            assert st[b] == 1, b
+    assert 0 in statuses
+
+
+def test_shared_point_equals_shared_problem(gpu_available):
+    """All instances at the reference's point: same solutions as the shared-problem kernels."""
+    import torch
+    from carmpc_amd.configuration import LINEARIZE_INPUT, LINEARIZE_STATE
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.hetero import MPCStateFBBatch
+    from carmpc_amd.mpc import MPCStateFB
+    B = 256
+    env = ENVIRONMENTS["RoadMultipleCarsEnv"]()
+    fleet = MPCStateFBBatch(0.2, 20, np.tile(LINEARIZE_STATE, (B, 1)), np.tile(LINEARIZE_INPUT, (B, 1)), env=env,
+                            terminal_set_dir=TERMINAL_SETS)
+    ctrl = MPCStateFB(dt=0.2, N=20, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT, env=env,
+                      terminal_set_dir=TERMINAL_SETS)
+    rng = np.random.default_rng(11)
+    x0 = torch.as_tensor(np.column_stack([rng.uniform(0, 28, B), rng.uniform(-2.5, 2.5, B),
+                                          rng.uniform(-0.3, 0.3, B), rng.uniform(0, 4, B)])).cuda()
+    _a, u1, s1 = fleet.step_batch(x0)
+    _b, u2, s2 = ctrl.step_batch(x0)
+    assert torch.equal(s1, s2)
+    ok = (s1 == 0)
+    assert float((u1[ok] - u2[ok]).abs().max()) <= 2 * U_TOL
+
+
+def test_relinearize_in_place(gpu_available):
+    import torch
+    fleet, ls, li = _fleet(8, 4)
+    m1 = fleet.model()
+    ls2 = ls.copy()
+    ls2[:, 3] += 1.0
+    fleet.relinearize(torch.as_tensor(ls2).cuda(), torch.as_tensor(li).cuda())
+    m2 = fleet.model()
+    assert not np.allclose(m1["B"], m2["B"])
+    fleet.relinearize(ls, li)
+    np.testing.assert_array_equal(fleet.model()["P"], m1["P"])
