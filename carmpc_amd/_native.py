@@ -27,7 +27,7 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
            "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
            "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
-           "carmpc_hetero_get")
+           "carmpc_hetero_get", "carmpc_set_serial_segments")
 
 # outcomes of carmpc_closed_loop_batch (carmpc.h)
 LOOP_RUNNING, LOOP_REACHED, LOOP_INFEASIBLE, LOOP_INPUT_VIOLATION, LOOP_TIMEOUT, LOOP_SOLVER_FAILURE = -1, 0, 1, 2, 3, 4
@@ -113,6 +113,7 @@ def load():
         "carmpc_hetero_destroy": ([vp], None),
         "carmpc_hetero_linearize": ([vp, vp, vp, vp], ctypes.c_int),
         "carmpc_hetero_solve": ([vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
+        "carmpc_set_serial_segments": ([i32], None),
         "carmpc_hetero_get": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "carmpc_closed_loop_batch": ([vp, i64, ctypes.POINTER(LoopDesc), vp, vp, vp, vp, vp, vp, vp, i32,
                                       ctypes.POINTER(Settings), vp], ctypes.c_int),

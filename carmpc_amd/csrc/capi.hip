@@ -85,6 +85,31 @@ struct carmpc_hetero {
 };
 
 namespace {
+// side streams of carmpc_solve_segments, one set per (thread, device)
+struct SideStreams {
+    static constexpr int kN = 4;
+    hipStream_t s[kN];
+    hipEvent_t fork, join[kN];
+};
+bool g_serial_segments = false;
+SideStreams* side_streams() {
+    thread_local SideStreams* per_dev[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!per_dev[dev]) {
+        auto* ss = new SideStreams();
+        for (int i = 0; i < SideStreams::kN; ++i) {
+            if (hipStreamCreateWithFlags(&ss->s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
+            if (hipEventCreateWithFlags(&ss->join[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+        }
+        if (hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+        per_dev[dev] = ss;
+    }
+    return per_dev[dev];
+}
+}  // namespace
+
+namespace {
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -663,21 +688,50 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
                           int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
     if (!probs || !offsets || nprobs < 0) return fail(CARMPC_EINVAL, "null argument");
     const Settings s = make_settings(settings);
+    int live = 0;
     for (int j = 0; j < nprobs; ++j) {
         const int64_t b0 = offsets[j], b1 = offsets[j + 1];
         if (b1 < b0) return fail(CARMPC_EINVAL, "offsets must be non-decreasing");
         if (b1 == b0) continue;
+        if (!probs[j]) return fail(CARMPC_EINVAL, "null problem in segment list");
+        if (ld_u < probs[j]->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
+        ++live;
+    }
+    // Several segments: fork them onto side streams so a launch's tail (groups finishing their
+    // last instances) overlaps the next segment's start, then join back into `stream`.
+    SideStreams* side = nullptr;
+    if (live > 1 && !g_serial_segments) {
+        side = side_streams();
+        if (!side) return hipfail(hipGetLastError(), "side streams");
+        HIP_TRY(hipEventRecord(side->fork, stream), "fork event");
+    }
+    int k = 0;
+    for (int j = 0; j < nprobs; ++j) {
+        const int64_t b0 = offsets[j], b1 = offsets[j + 1];
+        if (b1 == b0) continue;
         const carmpc_problem* P = probs[j];
-        if (!P) return fail(CARMPC_EINVAL, "null problem in segment list");
-        if (ld_u < P->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
+        hipStream_t sj = stream;
+        if (side) {
+            sj = side->s[k % SideStreams::kN];
+            HIP_TRY(hipStreamWaitEvent(sj, side->fork, 0), "side stream wait");
+        }
+        ++k;
         int unsupported = 0;
         hipError_t e = launch_solve(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
-                                    ld_u, status + b0, iters ? iters + b0 : nullptr, s, stream, &unsupported);
+                                    ld_u, status + b0, iters ? iters + b0 : nullptr, s, sj, &unsupported);
         if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
         if (e != hipSuccess) return hipfail(e, "segment launch");
     }
+    if (side) {
+        for (int i = 0; i < k && i < SideStreams::kN; ++i) {
+            HIP_TRY(hipEventRecord(side->join[i], side->s[i]), "join event");
+            HIP_TRY(hipStreamWaitEvent(stream, side->join[i], 0), "join wait");
+        }
+    }
     return CARMPC_OK;
 }
+
+void carmpc_set_serial_segments(int32_t serial) { g_serial_segments = serial != 0; }
 
 int carmpc_problem_set_disturbance(carmpc_problem* P, const double* Bd) {
     if (!P || !Bd) return fail(CARMPC_EINVAL, "null argument");

@@ -282,15 +282,21 @@ class QPProblem:
         return {"state": state, "xhat": xhat, "dhat": dhat, "u": u, "outcome": outcome, "steps": steps}
 
 def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,
-                   settings: SolverSettings | None = None, stream=None):
-    """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j]."""
+                   settings: SolverSettings | None = None, stream=None, out: tuple | None = None):
+    """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j].  The
+    segments' launches run concurrently on side streams, joined back into ``stream``.
+    ``out`` = (u (B x ld), status, iters) preallocated device tensors."""
     dev = problems[0].device
     x0 = _as_dev(x0, dev)
     B = x0.shape[0]
-    ld = max(p.n for p in problems)
-    u = torch.zeros((B, ld), dtype=torch.float64, device=dev)
-    st = torch.empty(B, dtype=torch.int32, device=dev)
-    it = torch.empty(B, dtype=torch.int32, device=dev)
+    if out is None:
+        ld = max(p.n for p in problems)
+        u = torch.zeros((B, ld), dtype=torch.float64, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        it = torch.empty(B, dtype=torch.int32, device=dev)
+    else:
+        u, st, it = out
+        ld = u.stride(0)
     handles = (ctypes.c_void_p * len(problems))(*[p._h.value for p in problems])
     offs = (ctypes.c_int64 * (len(problems) + 1))(*[int(o) for o in offsets])
     s = (settings or SolverSettings()).c()
@@ -300,8 +306,6 @@ def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor
                                                    _tptr(st), _tptr(it), ctypes.byref(s), _stream_handle(stream)),
               "carmpc_solve_segments")
     return u, st, it
-
-
 
 
 class HeteroQP:
