@@ -94,6 +94,7 @@ struct Settings {
     const double* dist;    // per-instance disturbance estimate d (device, batch) or nullptr
     const int32_t* index;  // slot -> instance row (device) or nullptr = identity
     const int32_t* count;  // number of slots (device scalar) or nullptr = batch
+    unsigned* claim;       // dynamic instance counter of one launch (zeroed), Riccati kernel; nullptr = static
 };
 
 

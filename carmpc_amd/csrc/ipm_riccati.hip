@@ -509,13 +509,19 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         wb();
     };
 
-    // Each group walks its own instance sequence (inst, inst + stride, ...) and starts the
-    // next instance at the first trip after finishing one, so the 4 groups of a wave never
-    // wait for the slowest instance (infeasible ones stop after a few iterations).
+    // Each group claims its next instance from the launch's counter (S.claim, one atomic per
+    // instance by the group's lane 0) at the first trip after finishing one, so the 4 groups
+    // of a wave never wait for the slowest instance and no group is left with a heavier static
+    // share at the end of the launch.  Without a counter: static stride over the grid.
     const int64_t stride = (int64_t)gridDim.x * WPB * 4;
+    auto claim = [&]() -> int64_t {
+        unsigned v = 0;
+        if (j == 0) v = atomicAdd(S.claim, 1u);
+        return (int64_t)__shfl(v, lane & ~(G16 - 1), 64);
+    };
     // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
     const int64_t nlive = S.count ? (int64_t)*S.count : batch;
-    int64_t slot = ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
+    int64_t slot = S.claim ? claim() : ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
     bool live = slot < nlive;   // the group has an instance to work on
     int64_t inst = live && S.index ? (int64_t)S.index[slot] : slot;
     bool fresh = true;          // ... that still needs its initial point
@@ -537,7 +543,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             status_out[inst] = st;
             if (iters_out) iters_out[inst] = it;
         }
-        slot += stride;
+        slot = S.claim ? claim() : slot + stride;
         live = slot < nlive;
         inst = live && S.index ? (int64_t)S.index[slot] : slot;
         fresh = true;
@@ -1288,9 +1294,24 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
         int64_t grid = (int64_t)cus * per_cu;
         if (want < grid) grid = want;
         if (grid < 1) grid = 1;
+        // per-launch claim counter, stream-ordered (allocated, zeroed, freed on `stream`)
+        Settings sc = s;
+        unsigned* counter = nullptr;
+        if (batch > 1) {
+            e = hipMallocAsync(reinterpret_cast<void**>(&counter), sizeof(unsigned), stream);
+            if (e != hipSuccess) return e;
+            e = hipMemsetAsync(counter, 0, sizeof(unsigned), stream);
+            if (e != hipSuccess) return e;
+            sc.claim = counter;
+        }
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
-                           status, iters, s);
-        return hipGetLastError();
+                           status, iters, sc);
+        e = hipGetLastError();
+        if (counter) {
+            const hipError_t ef = hipFreeAsync(counter, stream);
+            if (e == hipSuccess) e = ef;
+        }
+        return e;
     };
     const bool bike = P.ric == 2;
     switch (P.N) {
