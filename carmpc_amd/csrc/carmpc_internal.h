@@ -98,6 +98,31 @@ struct Settings {
 };
 
 
+// Dynamic instance claiming (one atomic per instance on a per-launch counter): the
+// wavefront-per-QP kernels take the next instance with wave_claim; the counter lives for one
+// launch, stream-ordered (launch_with_claim).
+__device__ __forceinline__ int64_t wave_claim(unsigned* c) {
+    unsigned v = 0;
+    if ((threadIdx.x & 63) == 0) v = atomicAdd(c, 1u);
+    return (int64_t)__builtin_amdgcn_readfirstlane(v);
+}
+template <class Launch>
+inline hipError_t launch_with_claim(Settings s, int64_t batch, hipStream_t stream, Launch&& launch) {
+    unsigned* counter = nullptr;
+    hipError_t e = hipSuccess;
+    if (batch > 1) {
+        if ((e = hipMallocAsync(reinterpret_cast<void**>(&counter), sizeof(unsigned), stream)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(counter, 0, sizeof(unsigned), stream)) != hipSuccess) return e;
+        s.claim = counter;
+    }
+    e = launch(s);
+    if (counter) {
+        const hipError_t ef = hipFreeAsync(counter, stream);
+        if (e == hipSuccess) e = ef;
+    }
+    return e;
+}
+
 // Argument blocks of the setup kernels (assembly.hip).
 struct AsmArgs {
     int N, nu, n, nt, ns;

@@ -229,7 +229,9 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
 
     // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
     const int64_t nlive = S.count ? (int64_t)*S.count : batch;
-    for (int64_t slot = (int64_t)blockIdx.x * kWPB + wave; slot < nlive; slot += (int64_t)gridDim.x * kWPB) {
+    const int64_t stride = (int64_t)gridDim.x * kWPB;
+    for (int64_t slot = S.claim ? wave_claim(S.claim) : (int64_t)blockIdx.x * kWPB + wave; slot < nlive;
+         slot = S.claim ? wave_claim(S.claim) : slot + stride) {
         const int64_t inst = S.index ? (int64_t)S.index[slot] : slot;
         // this instance's rows (shared problem: the launch's; HET: its own slice)
         const double *Pw0 = P.w0, *PE = P.E, *Phq = P.hq, *Ppw = P.pre_w0, *PpE = P.pre_E;
@@ -579,9 +581,11 @@ hipError_t launch_t(const DevProblem& P, int64_t batch, const double* x0, const 
     int64_t grid = (int64_t)cus * per_cu;
     if (want < grid) grid = want;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), lds, stream, P, batch, x0, xref, u_out, ld_u,
-                       status, iters, s);
-    return hipGetLastError();
+    return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), lds, stream, P, batch, x0, xref, u_out, ld_u,
+                           status, iters, sc);
+        return hipGetLastError();
+    });
 }
 
 template <int NV>
@@ -623,9 +627,11 @@ hipError_t launch_het_t(const DevProblem& P, int64_t batch, const double* x0, co
     int64_t grid = (int64_t)cus * per_cu;
     if (want < grid) grid = want;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
-                       status, iters, s);
-    return hipGetLastError();
+    return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kWPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
+                           status, iters, sc);
+        return hipGetLastError();
+    });
 }
 template <int NV>
 hipError_t launch_het_rs(int rs, const DevProblem& P, int64_t batch, const double* x0, const double* xref,

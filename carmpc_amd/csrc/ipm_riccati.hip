@@ -1295,23 +1295,11 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
         if (want < grid) grid = want;
         if (grid < 1) grid = 1;
         // per-launch claim counter, stream-ordered (allocated, zeroed, freed on `stream`)
-        Settings sc = s;
-        unsigned* counter = nullptr;
-        if (batch > 1) {
-            e = hipMallocAsync(reinterpret_cast<void**>(&counter), sizeof(unsigned), stream);
-            if (e != hipSuccess) return e;
-            e = hipMemsetAsync(counter, 0, sizeof(unsigned), stream);
-            if (e != hipSuccess) return e;
-            sc.claim = counter;
-        }
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
-                           status, iters, sc);
-        e = hipGetLastError();
-        if (counter) {
-            const hipError_t ef = hipFreeAsync(counter, stream);
-            if (e == hipSuccess) e = ef;
-        }
-        return e;
+        return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
+                               status, iters, sc);
+            return hipGetLastError();
+        });
     };
     const bool bike = P.ric == 2;
     switch (P.N) {
