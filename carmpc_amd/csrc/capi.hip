@@ -417,7 +417,7 @@ hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, co
 extern "C" {
 
 const char* carmpc_last_error(void) { return g_err.c_str(); }
-const char* carmpc_version(void) { return "carmpc-mi355x 0.2 (gfx950, dense + staged IPM)"; }
+const char* carmpc_version(void) { return "carmpc-mi355x 0.3 (gfx950: riccati / staged / dense IPM, closed loop, batched LP, per-instance linearisation)"; }
 
 int carmpc_problem_kernel(const carmpc_problem* P) {
     if (!P) return fail(CARMPC_EINVAL, "null problem");

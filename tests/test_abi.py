@@ -48,3 +48,11 @@ def test_build_entry_declares_gfx950():
                           os.path.join(REPO, "carmpc_amd", "libcarmpc.so")], capture_output=True, text=True)
     blob = open(os.path.join(REPO, "carmpc_amd", "libcarmpc.so"), "rb").read()
     assert b"gfx950" in blob
+
+
+def test_c_host_compiles(tmp_path):
+    """The header is plain C: a C host (examples/c_host) builds with gcc -Wall -Werror and links
+    the in-tree library."""
+    import c_host
+    exe = c_host.build(tmp_path)
+    assert os.path.exists(exe)
