@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(kWPB * 64) ipm_dense_kernel(DevProblem P, int6
 #pragma unroll
             for (int s = 0; s < RS; ++s) { ra[s] = 0.0; rb[s] = 0.0; pa[s] = 0.0; }
             double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, pua = 0.0, pla = 0.0, sigma_mu = 0.0;
-            const int nsolve = polish ? POLISH_REFINE + 1 : 3;
+            const int nsolve = polish ? POLISH_REFINE + 1 : (mu <= REFINE_MU ? 3 : 2);   // refinement late only
 #pragma unroll 1
             for (int k = 0; k < nsolve; ++k) {
                 double rhs, ryu = 0.0, ryl = 0.0;

@@ -890,20 +890,30 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             }
             // ================= solves =================
             // fully unrolled: k is a constant in every branch below (precise register lifetimes)
+            // the refinement solve (k = 2 of a normal trip) only once mu <= REFINE_MU; before
+            // that its correction is zero
+            const bool refine = mu <= REFINE_MU;
 #pragma unroll
             for (int k = 0; k < POLISH_REFINE + 1; ++k) {
                 if (k == 3 && !any_polish) break;
                 const bool run = active && (polish || k < 3);
-                if (k > 0 && run) back_linear();
+                const bool solve = run && (polish || k != 2 || refine);
+                if (k > 0 && solve) back_linear();
                 RT_MARK(6);
-                if (run) forward();
+                if (solve) forward();
                 RT_MARK(7);
                 if (!run) continue;
                 double dy[2][4], dv[2][2];
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg) {
-                    rd4((kseg[sg] - 1) * REC + O_BX, dy[sg]);
-                    rd2((kseg[sg] - 1) * REC + O_BU, dv[sg][0], dv[sg][1]);
+                    if (solve) {
+                        rd4((kseg[sg] - 1) * REC + O_BX, dy[sg]);
+                        rd2((kseg[sg] - 1) * REC + O_BU, dv[sg][0], dv[sg][1]);
+                    } else {
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) dy[sg][a] = 0.0;
+                        dv[sg][0] = dv[sg][1] = 0.0;
+                    }
                 }
                 wb();
                 if (polish) {
@@ -1145,6 +1155,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
+                    if (refine)
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
@@ -1160,7 +1171,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(-dz, c[aa], acc[sg][aa]);
                     }
                     wb();
-                    write_bx(acc, dy, -1.0);
+                    if (refine) write_bx(acc, dy, -1.0);
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg) {
                         const int t = kseg[sg] - 1;

@@ -29,6 +29,7 @@
 #define PRE_TOL 1e-9
 #define STEP_FRAC 0.99
 #define POLISH_MU 1e-8
+#define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
 #define POLISH_REFINE 3
 #define POLISH_TOL 1e-11
@@ -354,8 +355,9 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
                 dZu[i] = (-rcu[i] - zu[i] * dSu[i]) / su[i];
                 dZl[i] = (-rcl[i] - zl[i] * dSl[i]) / sl[i];
             }
-            if (pass == 1) {
-                /* refinement: e = H du + G'dz + box + rd ; M c = -e ; du += c, ds -= G c, dz += z G c / s */
+            if (pass == 1 && mu <= REFINE_MU) {
+                /* refinement (once mu <= REFINE_MU): e = H du + G'dz + box + rd ; M c = -e ;
+                   du += c, ds -= G c, dz += z G c / s */
                 double* e = W->nv5;
                 gtmul(P, dZ, e);
                 for (int i = 0; i < n; ++i) {

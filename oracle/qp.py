@@ -32,6 +32,7 @@ TOL_MU = 1e-12
 MAX_ITER = 60
 STEP_FRAC = 0.99
 REFINE = 1                 # iterative-refinement passes on the corrector direction
+REFINE_MU = 1e-6           # ... only once mu <= REFINE_MU (D = z/s spans many decades)
 POLISH_MU = 1e-8           # attempt the active-set polish once mu <= POLISH_MU (and residuals ok)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 3          # iterative-refinement passes of the polish
@@ -172,7 +173,7 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         smu = sigma * mu
         du, ds, dz, dsu, dzu, dsl, dzl = solve(s * z + ds * dz - smu, su * zu + dsu * dzu - smu,
                                                sl * zl + dsl * dzl - smu)
-        for _ in range(refine):
+        for _ in range(refine if mu <= REFINE_MU else 0):
             # residual of the dual equation H du + A'dz = -rd for the reconstructed direction;
             # correct with the same factor: M dU = -e, dS = -A dU, dZ = -z dS / s
             e = H @ du + G.T @ dz + rd + (box_T(dzu, dzl) if boxed else 0.0)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (MAX_ITER, POLISH_DELTA, POLISH_MU, POLISH_REFINE, POLISH_TOL, PRE_TOL, STEP_FRAC,
+from .qp import (MAX_ITER, POLISH_DELTA, POLISH_MU, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -240,15 +240,16 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER):
         rcu = (su * zu + dsu * dzu - smu) * bmask
         rcl = (sl * zl + dsl * dzl - smu) * bmask
         du, dy, ds, dz, dsu, dzu, dsl, dzl = solve(s * z + ds * dz - smu, rcu, rcl)
-        # refinement: e = H du + G'dz + rd + box;  M c = -e
-        bu = -(Rhat(du) + rd + (dzu - dzl) * bmask)
-        bx = -(sq.qbar_y(dy) + sq.stage_sum(dz))
-        cu, cy = sq.riccati_solve(fac, bu, bx)
-        cs = -sq.grow(cy)
-        du = du + cu; ds = ds + cs; dz = dz - z * cs / s
-        if boxed:
-            dsu = dsu - cu; dzu = dzu + zu * cu / su
-            dsl = dsl + cu; dzl = dzl - zl * cu / sl
+        if mu <= REFINE_MU:
+            # refinement: e = H du + G'dz + rd + box;  M c = -e
+            bu = -(Rhat(du) + rd + (dzu - dzl) * bmask)
+            bx = -(sq.qbar_y(dy) + sq.stage_sum(dz))
+            cu, cy = sq.riccati_solve(fac, bu, bx)
+            cs = -sq.grow(cy)
+            du = du + cu; ds = ds + cs; dz = dz - z * cs / s
+            if boxed:
+                dsu = dsu - cu; dzu = dzu + zu * cu / su
+                dsl = dsl + cu; dzl = dzl - zl * cu / sl
         ms = [_maxstep(s, ds), _maxstep(z, dz)]
         if boxed:
             ms += [_maxstep(su, dsu), _maxstep(zu, dzu), _maxstep(sl, dsl), _maxstep(zl, dzl)]
