@@ -16,6 +16,10 @@ SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_r
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-I" + os.path.join(REPO, "include")]
+# Per-file code generation: the Riccati kernel runs one wave per SIMD and is latency-bound in
+# its stage recursions; the iterative ILP scheduler gains ~3 % there (tools/gpu/sched_sweep.sh:
+# 6.71M -> 6.91M QP/s; max-ilp, max-memory-clause, iterative-minreg/maxocc were slower).
+FILE_FLAGS = {"ipm_riccati.hip": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]}
 
 
 def _hipcc():
@@ -29,7 +33,7 @@ def _stale(obj, src):
     if not os.path.exists(obj):
         return True
     deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h"),
-            os.path.join(REPO, "include", "carmpc.h")]
+            os.path.join(REPO, "include", "carmpc.h"), os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
@@ -46,7 +50,7 @@ def build(verbose: bool = True, jobs: int = 4, variant: str = "") -> str:
         s = os.path.join(CSRC, src)
         o = os.path.join(obj_dir, src.replace(".hip", ".o"))
         if _stale(o, s):
-            cmd = [hipcc, *FLAGS, *extra, "-c", s, "-o", o]
+            cmd = [hipcc, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
