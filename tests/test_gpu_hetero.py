@@ -138,3 +138,30 @@ def test_relinearize_in_place(gpu_available):
     assert not np.allclose(m1["B"], m2["B"])
     fleet.relinearize(ls, li)
     np.testing.assert_array_equal(fleet.model()["P"], m1["P"])
+
+
+@pytest.mark.parametrize("N,tsd", [(10, TERMINAL_SETS), (20, "/nonexistent")])
+def test_per_instance_other_horizon_and_goal_box(gpu_available, N, tsd):
+    """N = 10, and the goal-box terminal fallback (opposite row pairs, mpc.py:107-117)."""
+    import torch
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.hetero import MPCStateFBBatch
+    from oracle import assembly as oa
+    from oracle import qp as oq
+    B = 32
+    ls, li = _lin_points(B, 9)
+    fleet = MPCStateFBBatch(0.2, N, ls, li, env=ENVIRONMENTS["RoadMultipleCarsEnv"](), terminal_set_dir=tsd)
+    rng = np.random.default_rng(13)
+    x0 = fleet.goal + rng.normal(scale=0.4, size=(B, 4))
+    _u0, u, st = fleet.step_batch(torch.as_tensor(x0).cuda())
+    u, st = u.cpu().numpy(), st.cpu().numpy()
+    seen = 0
+    for b in range(B):
+        asm = oa.build("RoadMultipleCarsEnv", N, lin_state=ls[b], lin_input=li[b], terminal_set_dir=tsd)
+        r = oq.solve_instance(asm, x0[b])
+        if r["status"] == 0 and r["certified"]:
+            seen += 1
+            assert st[b] == 0 and np.abs(u[b] - r["u_exact"]).max() <= U_TOL, b
+        elif r["status"] == 1:
+            assert st[b] == 1, b
+    assert seen > 0
