@@ -63,8 +63,15 @@ struct carmpc_hetero {
     int32_t* lin_status = nullptr;
     double *G = nullptr, *H = nullptr, *hq = nullptr, *w0 = nullptr, *E = nullptr, *pw = nullptr, *pE = nullptr;
     int32_t *partner = nullptr, *p = nullptr, *npre = nullptr;
+    // Riccati path: the template problem's layout and per-instance slot data
+    carmpc_problem* tmpl = nullptr;
+    DevProblem ric{};     // template dev + per-instance slice pointers (ipm_riccati HET)
+    int32_t* tmpl_slot = nullptr;
+    double *ric_invn = nullptr, *ric_w0 = nullptr, *ric_E = nullptr;
+    int32_t *layout_ok = nullptr, *idx_ok = nullptr, *idx_bad = nullptr, *cnt = nullptr;
     ~carmpc_hetero() {
         for (void* q : allocs) (void)hipFree(q);
+        delete tmpl;
     }
     template <class T_>
     hipError_t alloc(T_** ptr, size_t count) {
@@ -411,6 +418,67 @@ hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, co
     const bool staged = (s.kernel >= 4 && s.kernel <= 6) || s.kernel == 2 || (s.kernel == 0 && D.staged);
     if (staged) return launch_staged(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     return launch_dense(D, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+}
+}  // namespace
+
+// Riccati layout for per-instance problems: a template problem with the same rows at a generic
+// linearisation point (v = 1: every input reaches the psi and v rows at stage 1) gives the slot of
+// every QP row; instances whose rows split the same way (layout_ok) run on the Riccati kernel, the
+// rest on the dense per-instance kernel.
+int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out);
+namespace {
+int hetero_riccati_template(carmpc_hetero* h, const carmpc_hetero_desc* d) {
+    const int N = d->N;
+    if (!riccati_supported_N(N)) return CARMPC_OK;
+    const double dt = d->dt, v = 1.0;
+    double A[16] = {1, 0, 0, dt, 0, 1, dt * v, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    double B[8] = {0, 0, 0, 0, 0, dt * v / d->l1, dt, 0};
+    double Pm[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    carmpc_model_desc md{};
+    md.N = N; md.nx = NX; md.nu = 2; md.A = A; md.B = B; md.Q = d->Q; md.R = d->R; md.P = Pm;
+    md.n_state_rows = d->n_state_rows; md.state_A = d->state_A; md.state_b = d->state_b;
+    md.n_term_rows = d->n_term_rows; md.term_A = d->term_A; md.term_b = d->term_b;
+    md.u_lower = d->u_lower; md.u_upper = d->u_upper; md.goal = d->goal;
+    carmpc_problem* T = nullptr;
+    const int rc = carmpc_problem_create(&md, &T);
+    if (rc != CARMPC_OK) return rc;
+    h->tmpl = T;
+    if (T->dev.ric != 2 || T->ric_slot.size() != T->qp_rows.size()) return CARMPC_OK;   // no bicycle layout
+    const int nt = d->n_term_rows, pa = h->p_all;
+    constexpr int kSlots = kRicSlots * kRicLanes;
+    std::vector<int32_t> slot_of_row(pa, -1);
+    std::vector<double> raw((size_t)kSlots * NX, 0.0);
+    for (size_t i = 0; i < T->qp_rows.size(); ++i) {
+        const int e = T->qp_rows[i], slot = T->ric_slot[i];
+        slot_of_row[e] = slot;
+        const double* c = e < nt ? d->term_A + (size_t)e * NX : d->state_A + (size_t)((e - nt) / N) * NX;
+        for (int a = 0; a < NX; ++a) raw[(size_t)slot * NX + a] = c[a];
+    }
+    const int64_t B_ = h->batch;
+    double* draw = nullptr;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t r) { if (e == hipSuccess) e = r; };
+    chk(h->upload(&h->tmpl_slot, slot_of_row.data(), slot_of_row.size()));
+    chk(h->upload(&draw, raw.data(), raw.size()));
+    chk(h->alloc(&h->ric_invn, (size_t)B_ * kSlots));
+    chk(h->alloc(&h->ric_w0, (size_t)B_ * kSlots));
+    chk(h->alloc(&h->ric_E, (size_t)B_ * kSlots * NX));
+    chk(h->alloc(&h->layout_ok, (size_t)B_));
+    chk(h->alloc(&h->idx_ok, (size_t)B_));
+    chk(h->alloc(&h->idx_bad, (size_t)B_));
+    chk(h->alloc(&h->cnt, 2));
+    if (e != hipSuccess) return hipfail(e, "hetero Riccati slices");
+    DevProblem R = T->dev;   // rows, slots, partners, box, Q, R of the template
+    R.r_coef = draw;         // raw row coefficients: the kernel scales them by each instance's 1/||G_r||
+    R.r_w0 = nullptr; R.r_E = nullptr;
+    R.hq = h->hq; R.pre_w0 = h->pw; R.pre_E = h->pE;
+    R.het_p = h->p; R.het_npre = h->npre;
+    R.het_sG = h->dev.het_sG; R.het_sH = h->dev.het_sH; R.het_sHq = h->dev.het_sHq; R.het_sRow = h->dev.het_sRow;
+    R.het_ric_invn = h->ric_invn; R.het_ric_w0 = h->ric_w0; R.het_ric_E = h->ric_E;
+    R.het_A = h->A; R.het_B = h->B; R.het_P = h->P;
+    R.Ed = R.pre_Ed = R.s_Ed = R.r_Ed = nullptr;
+    h->ric = R;
+    return CARMPC_OK;
 }
 }  // namespace
 
@@ -866,6 +934,11 @@ int carmpc_hetero_create(const carmpc_hetero_desc* d, int64_t batch, carmpc_hete
     D.G = h->G; D.H = h->H; D.hq = h->hq; D.w0 = h->w0; D.E = h->E; D.pre_w0 = h->pw; D.pre_E = h->pE;
     D.partner = h->partner; D.het_p = h->p; D.het_npre = h->npre;
     D.het_sG = sG; D.het_sH = sH; D.het_sHq = sHq; D.het_sRow = sRow;
+    const int rc = hetero_riccati_template(h, d);
+    if (rc != CARMPC_OK) {
+        delete h;
+        return rc;
+    }
     *out = h;
     return CARMPC_OK;
 }
@@ -885,7 +958,12 @@ int carmpc_hetero_linearize(carmpc_hetero* h, const double* lin_state, const dou
     a.G = h->G; a.H = h->H; a.hq = h->hq; a.w0 = h->w0; a.E = h->E; a.pre_w0 = h->pw; a.pre_E = h->pE;
     a.partner = h->partner; a.p = h->p; a.npre = h->npre;
     a.strideG = h->dev.het_sG; a.strideH = h->dev.het_sH; a.strideHq = h->dev.het_sHq; a.strideRow = h->dev.het_sRow;
+    a.tmpl_slot = h->tmpl_slot;
+    a.ric_invn = h->ric_invn; a.ric_w0 = h->ric_w0; a.ric_E = h->ric_E; a.layout_ok = h->layout_ok;
     HIP_TRY(launch_hetero_assembly(a, stream), "hetero assembly launch");
+    if (h->tmpl_slot)
+        HIP_TRY(launch_het_split(h->batch, h->layout_ok, h->idx_ok, h->cnt, h->idx_bad, h->cnt + 1, stream),
+                "hetero split");
     h->ready = true;
     return CARMPC_OK;
 }
@@ -897,8 +975,21 @@ int carmpc_hetero_solve(const carmpc_hetero* h, const double* x0, const double* 
     if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
     const Settings s = make_settings(settings);
     int unsupported = 0;
-    hipError_t e = launch_dense_het(h->dev, h->p_all, h->batch, x0, xref, u_out, h->dev.n, status, iters, s, stream,
-                                    &unsupported);
+    hipError_t e = hipSuccess;
+    if (h->tmpl_slot && (s.kernel == 0 || s.kernel == 7)) {
+        // Riccati kernel on the instances with the template's row layout, dense kernel on the rest
+        // (e.g. v = 0 linearisations, where the steering input leaves the psi rows at stage 1)
+        Settings so = s, sb = s;
+        so.index = h->idx_ok; so.count = h->cnt;
+        sb.index = h->idx_bad; sb.count = h->cnt + 1;
+        e = launch_riccati(h->ric, h->batch, x0, xref, u_out, h->dev.n, status, iters, so, stream, &unsupported, true);
+        if (e == hipSuccess && !unsupported)
+            e = launch_dense_het(h->dev, h->p_all, h->batch, x0, xref, u_out, h->dev.n, status, iters, sb, stream,
+                                 &unsupported);
+    } else {
+        e = launch_dense_het(h->dev, h->p_all, h->batch, x0, xref, u_out, h->dev.n, status, iters, s, stream,
+                             &unsupported);
+    }
     if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
     if (e != hipSuccess) return hipfail(e, "hetero solve launch");
     return CARMPC_OK;

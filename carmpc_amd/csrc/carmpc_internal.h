@@ -86,6 +86,9 @@ struct DevProblem {
     const int32_t* het_p;     // batch (nullptr: shared problem)
     const int32_t* het_npre;  // batch
     int64_t het_sG, het_sH, het_sHq, het_sRow;   // slice strides in elements
+    // per-instance Riccati layout (template slot map): 256 slots per instance
+    const double *het_ric_invn, *het_ric_w0, *het_ric_E;   // B x 256, B x 256, B x 256 x NX
+    const double *het_A, *het_B, *het_P;                    // B x 16, B x 8, B x 16
 };
 
 struct Settings {
@@ -210,9 +213,15 @@ struct HetAsmArgs {
     double *G, *H, *hq, *w0, *E, *pre_w0, *pre_E;
     int32_t *partner, *p, *npre;
     int64_t strideG, strideH, strideHq, strideRow;
+    // Riccati layout of the template (nullptr: none): slot of each assembled row, -1 = x0-only
+    const int32_t* tmpl_slot;
+    double *ric_invn, *ric_w0, *ric_E;   // B x 256, B x 256, B x 256 x NX
+    int32_t* layout_ok;                  // B: the instance splits its rows like the template
 };
 hipError_t launch_linearize(const LinArgs& a, hipStream_t s);
 hipError_t launch_hetero_assembly(const HetAsmArgs& a, hipStream_t s);
+hipError_t launch_het_split(int64_t batch, const int32_t* ok, int32_t* idx_ok, int32_t* cnt_ok, int32_t* idx_bad,
+                            int32_t* cnt_bad, hipStream_t s);
 hipError_t launch_dense_het(const DevProblem& P, int p_max, int64_t batch, const double* x0, const double* xref,
                             double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s,
                             hipStream_t stream, int* unsupported);
@@ -234,7 +243,7 @@ constexpr int kRicLanes = 16, kRicSeg = 8, kRicSlots = 2 * kRicSeg;
 bool riccati_supported_N(int N);
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref,
                           double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
-                          const Settings& s, hipStream_t stream, int* unsupported);
+                          const Settings& s, hipStream_t stream, int* unsupported, bool het = false);
 
 // Stage-structured kernel (ipm_staged.hip).
 constexpr int kStagedMaxRS = 4;

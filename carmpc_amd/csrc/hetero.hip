@@ -336,6 +336,48 @@ __global__ void __launch_bounds__(256) hetero_assembly_kernel(HetAsmArgs a) {
         }
         partner[r] = pr;
     }
+    // Riccati layout of the template: per-slot 1/||G_r||, w0 / ||G_r||, E / ||G_r|| (unused slots 0)
+    if (a.tmpl_slot) {
+        constexpr int kSlots = kRicSlots * kRicLanes;
+        double* iv = a.ric_invn + b * kSlots;
+        double* rw = a.ric_w0 + b * kSlots;
+        double* rE = a.ric_E + b * kSlots * 4;
+        for (int e = tid; e < kSlots; e += blockDim.x) {
+            iv[e] = 0.0;
+            rw[e] = 0.0;
+            for (int y = 0; y < 4; ++y) rE[e * 4 + y] = 0.0;
+        }
+        __syncthreads();
+        const double thr = ZERO_ROW * [&] {
+            double mx = 0.0;
+            for (int e = 0; e < p_all; ++e) mx = fmax(mx, nrm[e]);
+            return mx;
+        }();
+        int bad = 0;
+        for (int e = tid; e < p_all; e += blockDim.x) {
+            const bool qp = nrm[e] > thr;
+            const int slot = a.tmpl_slot[e];
+            if (qp != (slot >= 0)) {
+                bad = 1;
+                continue;
+            }
+            if (!qp) continue;
+            int st;
+            const double* c;
+            double bb;
+            row(e, &st, &c, &bb);
+            const double inv = 1.0 / nrm[e];
+            iv[slot] = inv;
+            rw[slot] = bb * inv;
+            for (int y = 0; y < 4; ++y) {
+                double v = 0.0;
+                for (int q = 0; q < 4; ++q) v += c[q] * Ap[st * 16 + q * 4 + y];
+                rE[slot * 4 + y] = v * inv;
+            }
+        }
+        bad = __syncthreads_or(bad);
+        if (tid == 0) a.layout_ok[b] = bad ? 0 : 1;
+    }
     for (int r = tid; r < np; r += blockDim.x) {
         const int e = pre_of[r];
         int st;
@@ -351,7 +393,27 @@ __global__ void __launch_bounds__(256) hetero_assembly_kernel(HetAsmArgs a) {
     }
 }
 
+// split the instances into those the Riccati kernel takes (template layout) and the rest
+__global__ void het_split_kernel(int64_t batch, const int32_t* ok, int32_t* idx_ok, int32_t* cnt_ok, int32_t* idx_bad,
+                                 int32_t* cnt_bad) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    if (ok[b]) idx_ok[atomicAdd(cnt_ok, 1)] = (int32_t)b;
+    else idx_bad[atomicAdd(cnt_bad, 1)] = (int32_t)b;
+}
+
 }  // namespace
+
+hipError_t launch_het_split(int64_t batch, const int32_t* ok, int32_t* idx_ok, int32_t* cnt_ok, int32_t* idx_bad,
+                            int32_t* cnt_bad, hipStream_t s) {
+    if (batch <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(cnt_ok, 0, sizeof(int32_t), s);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt_bad, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(het_split_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, batch, ok, idx_ok,
+                       cnt_ok, idx_bad, cnt_bad);
+    return hipGetLastError();
+}
 
 hipError_t launch_linearize(const LinArgs& a, hipStream_t s) {
     if (a.batch <= 0) return hipSuccess;

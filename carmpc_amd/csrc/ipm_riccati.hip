@@ -21,6 +21,8 @@
 #include "carmpc_internal.h"
 #include "lanes.h"
 
+#include <type_traits>
+
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -138,7 +140,35 @@ struct Mt {
     __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, -0.0)); }
 };
 
-template <int N, int WPB, class SP>
+// Per-instance model (carmpc_hetero_*): A, B of the group's own instance in registers (only the
+// entries inside the sparsity masks are ever read), Q, R shared from the kernel argument.
+template <class SP>
+struct MtH {
+    const StageMats& m;
+    double A[16], B[8];
+    __device__ explicit MtH(const StageMats& s) : m(s), A{}, B{} {}
+    __device__ __forceinline__ double A_(int a, int b, double x, double acc) const {
+        if (!((SP::A >> (a * 4 + b)) & 1u)) return acc;
+        if (SP::AUNIT && a == b) return acc + x;
+        return fma(A[a * 4 + b], x, acc);
+    }
+    __device__ __forceinline__ double B_(int a, int c, double x, double acc) const {
+        return ((SP::B >> (a * 2 + c)) & 1u) ? fma(B[a * 2 + c], x, acc) : acc;
+    }
+    __device__ __forceinline__ double Q_(int a, int b, double x, double acc) const {
+        return ((SP::Q >> (a * 4 + b)) & 1u) ? fma(m.Q[a * 4 + b], x, acc) : acc;
+    }
+    __device__ __forceinline__ double R_(int c, int d, double x, double acc) const {
+        return ((SP::R >> (c * 2 + d)) & 1u) ? fma(m.R[c * 2 + d], x, acc) : acc;
+    }
+    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : -0.0; }
+    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : -0.0; }
+    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, -0.0)); }
+};
+
+// HET: every instance has its own linearisation (hetero.hip): A, B, P, slot row norms, w0, E,
+// hq and x0-only rows come from the instance's slices; the row layout is the template's.
+template <int N, int WPB, class SP, bool HET = false>
 __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int64_t batch, const double* __restrict__ x0,
                                                                const double* __restrict__ xref, double* __restrict__ u_out,
                                                                int64_t ld_u, int32_t* __restrict__ status_out,
@@ -146,7 +176,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
     __shared__ __attribute__((aligned(16))) RicWave<N> wscr[WPB];
     const StageMats& MT = P.mats;
-    const Mt<SP> M{P.mats};
+    std::conditional_t<HET, MtH<SP>, const Mt<SP>> M{P.mats};
+    int64_t hinst = 0;   // HET: the group's current instance (slice index)
     for (int i = threadIdx.x; i < RS * G16; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.r_coef[i * 4 + 0], P.r_coef[i * 4 + 1]);
         sh.cf23[i] = make_double2(P.r_coef[i * 4 + 2], P.r_coef[i * 4 + 3]);
@@ -192,6 +223,16 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto cf = [&](int s, double (&c)[4]) {
         const double2 a = sh.cf01[s * G16 + j], b = sh.cf23[s * G16 + j];
         c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y;
+        if constexpr (HET) {   // raw template coefficients x this instance's 1/||G_r||
+            const double iv = P.het_ric_invn[hinst * (RS * G16) + s * G16 + j];
+#pragma unroll
+            for (int a2 = 0; a2 < 4; ++a2) c[a2] *= iv;
+        }
+    };
+    // terminal cost P (upper triangle read): shared, or this instance's DARE solution
+    auto Pv = [&](int idx) -> double {
+        if constexpr (HET) return P.het_P[hinst * 16 + idx];
+        else return MT.P[idx];
     };
     auto dot4 = [&](const double (&c)[4], const double (&y)[4]) {
         return fma(c[3], y[3], fma(c[2], y[2], fma(c[1], y[1], c[0] * y[0])));
@@ -225,7 +266,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             double accp = -0.0, accq = -0.0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                accp = fma(MT.P[(a < b ? a : b) * 4 + (a < b ? b : a)], v[b], accp);
+                accp = fma(Pv((a < b ? a : b) * 4 + (a < b ? b : a)), v[b], accp);
                 accq = M.Q_(a, b, v[b], accq);
             }
             y[a] = fma(sgn, termN ? accp : accq, y[a]);
@@ -383,7 +424,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = a; b < 4; ++b) Pm[sym10(a, b)] = MT.P[a * 4 + b] + Wn[sym10(a, b)];
+                for (int b = a; b < 4; ++b) Pm[sym10(a, b)] = Pv(a * 4 + b) + Wn[sym10(a, b)];
             rd4((N - 1) * REC + O_BX, pv);
         }
         // stage data one stage ahead: Db_t, b^u_t (record t), W_t, b^x_t (record t-1)
@@ -554,6 +595,20 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         RT_MARK(11);
         if (live && fresh) {
             fresh = false;
+            // this instance's data (HET) / the launch's problem
+            const double *Ipw = P.pre_w0, *IpE = P.pre_E, *Irw = P.r_w0, *IrE = P.r_E, *Ihq = P.hq;
+            if constexpr (HET) {
+                hinst = inst;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) M.A[e] = P.het_A[inst * 16 + e];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) M.B[e] = P.het_B[inst * 8 + e];
+                Ipw += inst * P.het_sRow;
+                IpE += inst * P.het_sRow * NX;
+                Irw = P.het_ric_w0 + inst * (RS * G16);
+                IrE = P.het_ric_E + inst * (RS * G16) * NX;
+                Ihq += inst * P.het_sHq;
+            }
             double xv0[NX], xr[NX];
 #pragma unroll
             for (int k = 0; k < NX; ++k) {
@@ -564,9 +619,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
             double bad = 0.0;
             for (int r = j; r < P.npre; r += G16) {
-                double v = P.pre_w0[r];
+                double v = Ipw[r];
 #pragma unroll
-                for (int k = 0; k < NX; ++k) v -= P.pre_E[r * NX + k] * xv0[k];
+                for (int k = 0; k < NX; ++k) v -= IpE[r * NX + k] * xv0[k];
                 if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
                 bad = v < -PRE_TOL ? 1.0 : bad;
             }
@@ -583,9 +638,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     double v = 0.0;
                     if (rv[s]) {
                         const int e = s * G16 + j;
-                        v = P.r_w0[e];
+                        v = Irw[e];
 #pragma unroll
-                        for (int k = 0; k < NX; ++k) v -= P.r_E[e * NX + k] * xv0[k];
+                        for (int k = 0; k < NX; ++k) v -= IrE[e * NX + k] * xv0[k];
                         if (P.r_Ed) v -= P.r_Ed[e] * dd;
                     }
                     wv.w[s][lane] = v;
@@ -599,7 +654,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                         const int i = 2 * t + c;
                         double q = 0.0;
 #pragma unroll
-                        for (int k = 0; k < NX; ++k) q = fma(P.hq[i * NX + k], xv0[k] - xr[k], q);
+                        for (int k = 0; k < NX; ++k) q = fma(Ihq[i * NX + k], xv0[k] - xr[k], q);
                         const double lb = sh.lb[i], ub = sh.ub[i];
                         const bool bx = own[sg] && boxed;
                         const double u0 = bx ? fmin(fmax(0.0, lb), ub) : 0.0;
@@ -1283,7 +1338,7 @@ bool riccati_supported_N(int N) { return N == 10 || N == 20; }
 
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
                           int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
-                          int* unsupported) {
+                          int* unsupported, bool het) {
     *unsupported = 0;
     if (batch <= 0) return hipSuccess;
     if (!P.ric) {
@@ -1313,6 +1368,17 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
         });
     };
     const bool bike = P.ric == 2;
+    if (het) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
+        if (!bike) {
+            *unsupported = 1;
+            return hipErrorInvalidValue;
+        }
+        switch (P.N) {
+            case 10: return go(ipm_riccati_kernel<10, WPB, BicycleModel, true>);
+            case 20: return go(ipm_riccati_kernel<20, WPB, BicycleModel, true>);
+            default: *unsupported = 1; return hipErrorInvalidValue;
+        }
+    }
     switch (P.N) {
         case 10: return bike ? go(ipm_riccati_kernel<10, WPB, BicycleModel>) : go(ipm_riccati_kernel<10, WPB, DenseModel>);
         case 20: return bike ? go(ipm_riccati_kernel<20, WPB, BicycleModel>) : go(ipm_riccati_kernel<20, WPB, DenseModel>);

@@ -165,3 +165,32 @@ def test_per_instance_other_horizon_and_goal_box(gpu_available, N, tsd):
         elif r["status"] == 1:
             assert st[b] == 1, b
     assert seen > 0
+
+
+def test_riccati_and_dense_per_instance_paths_agree(gpu_available):
+    """Default (Riccati kernel on the template row layout, dense kernel for the rest) vs the dense
+    per-instance kernel for all; a batch mixing v = 0 linearisations (other row layout)."""
+    import torch
+    from carmpc_amd.qp import SolverSettings
+    from oracle import assembly as oa
+    from oracle import qp as oq
+    B = 64
+    fleet, ls, li = _fleet(B, 21)
+    ls[5:9, 3] = 0.0                       # heading rows at stage 1 become x0-only rows
+    fleet.relinearize(ls, li)
+    rng = np.random.default_rng(17)
+    x0 = fleet.goal + rng.normal(scale=0.5, size=(B, 4))
+    X = torch.as_tensor(x0).cuda()
+    u1, s1, _ = fleet.qp.solve(X)
+    u2, s2, _ = fleet.qp.solve(X, settings=SolverSettings(kernel=1))
+    u1, s1, u2, s2 = (t.cpu().numpy() for t in (u1, s1, u2, s2))
+    np.testing.assert_array_equal(s1, s2)
+    ok = s1 == 0
+    assert np.abs(u1[ok] - u2[ok]).max() <= 2 * U_TOL
+    for b in list(range(4, 10)) + [0, 30]:
+        asm = oa.build("RoadMultipleCarsEnv", 20, lin_state=ls[b], lin_input=li[b], terminal_set_dir=TERMINAL_SETS)
+        r = oq.solve_instance(asm, x0[b])
+        if r["status"] == 0 and r["certified"]:
+            assert s1[b] == 0 and np.abs(u1[b] - r["u_exact"]).max() <= U_TOL, b
+        elif r["status"] == 1:
+            assert s1[b] == 1, b
