@@ -69,7 +69,7 @@ constexpr int REC = 20;   // doubles per stage record (160 B)
 //   [18..19] Db_t | kappa_t
 constexpr int O_K = 0, O_CH = 8, O_BX = 12, O_BU = 16, O_DB = 18;
 
-constexpr double POLISH_MU = 1e-8;
+constexpr double POLISH_MU = 1e-6;
 constexpr double POLISH_DELTA = 1e-10;
 constexpr int POLISH_REFINE = 3;
 constexpr double POLISH_TOL = 1e-11;

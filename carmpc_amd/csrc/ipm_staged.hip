@@ -57,7 +57,7 @@ namespace carmpc {
 
 namespace {
 
-constexpr double POLISH_MU = 1e-8;
+constexpr double POLISH_MU = 1e-6;
 constexpr double POLISH_DELTA = 1e-10;
 constexpr int POLISH_REFINE = 3;
 constexpr double POLISH_TOL = 1e-11;

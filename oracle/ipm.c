@@ -28,7 +28,7 @@
 #define UNBOXED_BOUND 1e9
 #define PRE_TOL 1e-9
 #define STEP_FRAC 0.99
-#define POLISH_MU 1e-8
+#define POLISH_MU 1e-6
 #define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
 #define POLISH_REFINE 3

@@ -33,7 +33,7 @@ MAX_ITER = 60
 STEP_FRAC = 0.99
 REFINE = 1                 # iterative-refinement passes on the corrector direction
 REFINE_MU = 1e-6           # ... only once mu <= REFINE_MU (D = z/s spans many decades)
-POLISH_MU = 1e-8           # attempt the active-set polish once mu <= POLISH_MU (and residuals ok)
+POLISH_MU = 1e-6           # attempt the active-set polish once mu <= POLISH_MU (and residuals ok)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 3          # iterative-refinement passes of the polish
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
