@@ -767,13 +767,21 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
     }
     // Several segments: fork them onto side streams so a launch's tail (groups finishing their
     // last instances) overlaps the next segment's start, then join back into `stream`.
+    // The claim counters of all segments are zeroed by one fill on `stream` before the fork: a
+    // fill on a side stream would queue behind the first segment's kernel (which holds every CU)
+    // and hold its own segment back until that kernel drains (seen in the v10 kernel trace).
     SideStreams* side = nullptr;
+    unsigned* counters = nullptr;
+    constexpr int kCounterStride = 16;   // one 64-B line per segment counter
     if (live > 1 && !g_serial_segments) {
         side = side_streams();
         if (!side) return hipfail(hipGetLastError(), "side streams");
+        const size_t bytes = sizeof(unsigned) * kCounterStride * live;
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&counters), bytes, stream), "segment counters");
+        HIP_TRY(hipMemsetAsync(counters, 0, bytes, stream), "zero segment counters");
         HIP_TRY(hipEventRecord(side->fork, stream), "fork event");
     }
-    int k = 0;
+    int k = 0, rc = CARMPC_OK;
     for (int j = 0; j < nprobs; ++j) {
         const int64_t b0 = offsets[j], b1 = offsets[j + 1];
         if (b1 == b0) continue;
@@ -783,20 +791,26 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
             sj = side->s[k % SideStreams::kN];
             HIP_TRY(hipStreamWaitEvent(sj, side->fork, 0), "side stream wait");
         }
+        Settings sk = s;
+        if (counters) sk.claim = counters + kCounterStride * k;
         ++k;
         int unsupported = 0;
         hipError_t e = launch_solve(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
-                                    ld_u, status + b0, iters ? iters + b0 : nullptr, s, sj, &unsupported);
-        if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
-        if (e != hipSuccess) return hipfail(e, "segment launch");
+                                    ld_u, status + b0, iters ? iters + b0 : nullptr, sk, sj, &unsupported);
+        if (unsupported || e != hipSuccess) {   // join what was queued, then report
+            rc = unsupported ? fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size")
+                             : hipfail(e, "segment launch");
+            break;
+        }
     }
     if (side) {
         for (int i = 0; i < k && i < SideStreams::kN; ++i) {
             HIP_TRY(hipEventRecord(side->join[i], side->s[i]), "join event");
             HIP_TRY(hipStreamWaitEvent(stream, side->join[i], 0), "join wait");
         }
+        HIP_TRY(hipFreeAsync(counters, stream), "free segment counters");
     }
-    return CARMPC_OK;
+    return rc;
 }
 
 void carmpc_set_serial_segments(int32_t serial) { g_serial_segments = serial != 0; }

@@ -104,7 +104,8 @@ struct Settings {
 
 // Dynamic instance claiming (one atomic per instance on a per-launch counter): the
 // wavefront-per-QP kernels take the next instance with wave_claim; the counter lives for one
-// launch, stream-ordered (launch_with_claim).
+// launch, stream-ordered (launch_with_claim), unless the caller already set s.claim to a zeroed
+// counter of its own (carmpc_solve_segments zeroes all segments' counters before its fork).
 __device__ __forceinline__ int64_t wave_claim(unsigned* c) {
     unsigned v = 0;
     if ((threadIdx.x & 63) == 0) v = atomicAdd(c, 1u);
@@ -114,7 +115,7 @@ template <class Launch>
 inline hipError_t launch_with_claim(Settings s, int64_t batch, hipStream_t stream, Launch&& launch) {
     unsigned* counter = nullptr;
     hipError_t e = hipSuccess;
-    if (batch > 1) {
+    if (batch > 1 && !s.claim) {
         if ((e = hipMallocAsync(reinterpret_cast<void**>(&counter), sizeof(unsigned), stream)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(counter, 0, sizeof(unsigned), stream)) != hipSuccess) return e;
         s.claim = counter;
