@@ -52,6 +52,17 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #define RT_FLUSH() do {} while (0)
 #endif
 
+// Unroll factor of the software-pipelined stage loops (forward, backward, roll-out,
+// factorization; adjoint pass): > 1 lets the compiler rename the one-stage-ahead prefetch
+// registers instead of copying them every stage.  Bench (1 GPU, QP/s) for unroll 1 / 2 / 4 /
+// 5 / 10 of both: 7.05M / 7.52M / 7.73M / 7.80M / 7.76M (tools/gpu/sched_sweep.sh variants).
+#ifndef CARMPC_RIC_UNROLL
+#define CARMPC_RIC_UNROLL 5
+#endif
+#ifndef CARMPC_RIC_UNROLL_ADJ
+#define CARMPC_RIC_UNROLL_ADJ 5
+#endif
+
 namespace carmpc {
 
 namespace {
@@ -309,7 +320,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         };
         double bu[2], ch[4], K[8], bx[4];
         ld(N - 1, bu, ch, K, bx);
-#pragma unroll 1
+#pragma unroll CARMPC_RIC_UNROLL
         for (int t = N - 1; t >= 0; --t) {
             double nbu[2], nch[4], nK[8], nbx[4];
             ld(t >= 1 ? t - 1 : 0, nbu, nch, nK, nbx);
@@ -352,7 +363,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         double K[8], kp[2];
         rdK(0, K);
         rd2(O_DB, kp[0], kp[1]);
-#pragma unroll 1
+#pragma unroll CARMPC_RIC_UNROLL
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             const int rn = (t + 1 < N ? t + 1 : t) * REC;
@@ -391,7 +402,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto rollout = [&]() {
         wb();
         double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
+#pragma unroll CARMPC_RIC_UNROLL
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             double v0, v1;
@@ -438,7 +449,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         };
         double du[4], Wt[10], bx[4];
         ld(N - 1, du, Wt, bx);
-#pragma unroll 1
+#pragma unroll CARMPC_RIC_UNROLL
         for (int t = N - 1; t >= 0; --t) {
             const int r = t * REC;
             double ndu[4], nWt[10], nbx[4];
@@ -767,7 +778,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     double lzv[4], lhv[4];
                     rd4((N - 1) * REC + 0, lzv);
                     rd4((N - 1) * REC + 4, lhv);
-#pragma unroll 1
+#pragma unroll CARMPC_RIC_UNROLL_ADJ
                     for (int t = N - 1; t >= 0; --t) {
                         const int r = t * REC;
                         double nlz[4], nlh[4];
