@@ -62,6 +62,10 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #ifndef CARMPC_RIC_UNROLL_ADJ
 #define CARMPC_RIC_UNROLL_ADJ 5
 #endif
+#ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
+                                // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
+#define CARMPC_RIC_UNROLL_HET 1
+#endif
 
 namespace carmpc {
 
@@ -184,6 +188,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                                                                const double* __restrict__ xref, double* __restrict__ u_out,
                                                                int64_t ld_u, int32_t* __restrict__ status_out,
                                                                int32_t* __restrict__ iters_out, Settings S) {
+    constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
+    constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
     __shared__ __attribute__((aligned(16))) RicWave<N> wscr[WPB];
     const StageMats& MT = P.mats;
@@ -320,7 +326,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         };
         double bu[2], ch[4], K[8], bx[4];
         ld(N - 1, bu, ch, K, bx);
-#pragma unroll CARMPC_RIC_UNROLL
+#pragma unroll kUnroll
         for (int t = N - 1; t >= 0; --t) {
             double nbu[2], nch[4], nK[8], nbx[4];
             ld(t >= 1 ? t - 1 : 0, nbu, nch, nK, nbx);
@@ -363,7 +369,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         double K[8], kp[2];
         rdK(0, K);
         rd2(O_DB, kp[0], kp[1]);
-#pragma unroll CARMPC_RIC_UNROLL
+#pragma unroll kUnroll
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             const int rn = (t + 1 < N ? t + 1 : t) * REC;
@@ -402,7 +408,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     auto rollout = [&]() {
         wb();
         double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll CARMPC_RIC_UNROLL
+#pragma unroll kUnroll
         for (int t = 0; t < N; ++t) {
             const int r = t * REC;
             double v0, v1;
@@ -449,7 +455,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         };
         double du[4], Wt[10], bx[4];
         ld(N - 1, du, Wt, bx);
-#pragma unroll CARMPC_RIC_UNROLL
+#pragma unroll kUnroll
         for (int t = N - 1; t >= 0; --t) {
             const int r = t * REC;
             double ndu[4], nWt[10], nbx[4];
@@ -778,7 +784,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     double lzv[4], lhv[4];
                     rd4((N - 1) * REC + 0, lzv);
                     rd4((N - 1) * REC + 4, lhv);
-#pragma unroll CARMPC_RIC_UNROLL_ADJ
+#pragma unroll kUnrollAdj
                     for (int t = N - 1; t >= 0; --t) {
                         const int r = t * REC;
                         double nlz[4], nlh[4];
