@@ -171,19 +171,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
-    # end-to-end (PCIe-inclusive) figure: H2D x0, solve, D2H u -- reported, never `value`
+    # end-to-end (PCIe-inclusive) figure: H2D x0, solve, D2H u and status between pinned host
+    # buffers, mean of 3 passes -- reported, never `value`
     Xh = torch.as_tensor(X).pin_memory()
+    uh = torch.empty(u.shape, dtype=u.dtype).pin_memory()
+    sh = torch.empty(st.shape, dtype=st.dtype).pin_memory()
+    Xe = torch.empty_like(Xh, device=device)
     torch.cuda.synchronize()
     te = time.perf_counter()
-    Xe = Xh.to(device, non_blocking=True)
-    if args.serial_segments:
-        for p, sl in segs:
-            p.solve(Xe[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
-    else:
-        solve_segments(probs, offsets, Xe, settings=settings, stream=stream, out=(u, st, it))
-    uh = u.to("cpu"); sh = st.to("cpu")
+    for _ in range(3):
+        with torch.cuda.stream(stream):
+            Xe.copy_(Xh, non_blocking=True)
+        if args.serial_segments:
+            for p, sl in segs:
+                p.solve(Xe[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
+        else:
+            solve_segments(probs, offsets, Xe, settings=settings, stream=stream, out=(u, st, it))
+        with torch.cuda.stream(stream):
+            uh.copy_(u, non_blocking=True)
+            sh.copy_(st, non_blocking=True)
     torch.cuda.synchronize()
-    e2e = B / (time.perf_counter() - te)
+    e2e = 3 * B / (time.perf_counter() - te)
 
     st_np = st.cpu().numpy(); it_np = it.cpu().numpy()
     if rank != 0:
