@@ -62,6 +62,14 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #ifndef CARMPC_RIC_UNROLL_ADJ
 #define CARMPC_RIC_UNROLL_ADJ 5
 #endif
+// Stage records: all 16 lanes of a group hold bitwise-identical values (redundant scalar
+// recursions), and every lane stores them (same address, same bits) -- no exec-mask branch
+// per stage.  Lane-0-only stores (CARMPC_RIC_LANE0_WRITE) measured 7.81M vs 8.05M QP/s.
+#ifdef CARMPC_RIC_LANE0_WRITE
+#define RIC_WRITER (j == 0)
+#else
+#define RIC_WRITER true
+#endif
 #ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
                                 // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
 #define CARMPC_RIC_UNROLL_HET 1
@@ -341,7 +349,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             const double y1 = fma(-l10, y0, g1) * il11;
             const double k1 = y1 * il11;
             const double k0 = fma(-l10, k1, y0) * il00;
-            if (j == 0) wr2(t * REC + O_DB, k0, k1);
+            if (RIC_WRITER) wr2(t * REC + O_DB, k0, k1);
             double np[4];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
@@ -393,7 +401,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             }
 #pragma unroll
             for (int a = 0; a < 4; ++a) y[a] = ny[a];
-            if (j == 0) {
+            if (RIC_WRITER) {
                 wr4(r + O_BX, y);
                 wr2(r + O_BU, v0, v1);
             }
@@ -425,7 +433,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
             for (int a = 0; a < 4; ++a) y[a] = ny[a];
             wb();
-            if (j == 0) wr4(r + O_BX, y);
+            if (RIC_WRITER) wr4(r + O_BX, y);
         }
         wb();
     };
@@ -516,7 +524,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
             const double k1 = y1 * il11;
             const double k0 = fma(-l10, k1, y0) * il00;
             wb();
-            if (j == 0) {
+            if (RIC_WRITER) {
                 wr4(r + O_K, K[0]);
                 wr4(r + O_K + 4, K[1]);
                 wr2(r + O_CH, il00, l10);
@@ -819,7 +827,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                             lo += fmin(az * lb, az * ub);
                             scf = fma(fabs(az), fmax(fabs(lb), fabs(ub)), scf);
                         }
-                        if (j == 0) {
+                        if (RIC_WRITER) {
                             wr2(r + 12, gz[0], gz[1]);
                             wr2(r + 14, hs[0], hs[1]);
                         }
