@@ -14,7 +14,11 @@ OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libcarmpc.so")
 SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip"]
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
+# -packed-fp32-ops off: hipcc -O3 forms v_pk_*_f32 from ordinary float code by itself and some of
+# their forms have given wrong results on these GPUs; the flag only concerns the device pass (the
+# host pass warns that it does not know the feature, which is harmless).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
          "-I" + os.path.join(REPO, "include")]
 # Per-file code generation: the Riccati kernel runs one wave per SIMD and is latency-bound in
 # its stage recursions; the iterative ILP scheduler gains ~3 % there (tools/gpu/sched_sweep.sh:

@@ -192,10 +192,16 @@ __global__ void plant_kernel(int64_t batch, double* state, const double* u, int6
     state[b * 4 + 1] = v * sin(psi) * dt + y;
     state[b * 4 + 2] = v / l1 * t * dt + psi;
     state[b * 4 + 3] = acc * dt + v;
-    if (bad) {
-        const double acc_hi = 2.0 + 0.05, del_hi = M_PI / 4 + 0.05;   // simulator.py:28-29
-        bad[b] = (acc > acc_hi || -acc > acc_hi || delta > del_hi || -delta > del_hi) ? 1 : 0;
-    }
+    if (bad) bad[b] = input_rejected(acc, delta) ? 1 : 0;
+}
+
+__global__ void zero_u32_kernel(unsigned* ptr, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) ptr[i] = 0u;
+}
+hipError_t launch_zero_u32(unsigned* ptr, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(zero_u32_kernel, dim3(1), dim3(64), 0, s, ptr, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_assembly(const AsmArgs& a, hipStream_t s) {

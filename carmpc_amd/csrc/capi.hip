@@ -11,12 +11,15 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "carmpc_internal.h"
 
 using namespace carmpc;
+
 
 struct carmpc_problem {
     DevProblem dev{};
@@ -35,8 +38,20 @@ struct carmpc_problem {
     std::vector<double> nrm_all;            // p_all condensed row norms
     std::vector<int32_t> qp_rows, pre_rows; // packed QP rows / x0-only rows (assembled indices)
     std::vector<int32_t> stage_slot, ric_slot;   // slot of each packed row per layout (empty: none)
+    // Observer constants (C, L | Cd, L2, Bd) staged on the device once per distinct value set
+    // (carmpc_problem_set_observer, or the first carmpc_observer*_batch call that passes them):
+    // later calls with the same host values only launch.  Superseded sets stay allocated until the
+    // problem is destroyed, so a launch still queued on some stream never loses its operands.
+    static constexpr int kObsStage = 2 * 8 * NX + 8 + 8 + NX;   // C 8xNX | L NXx8 | Cd 8 | L2 8 | Bd NX
+    struct ObsSet {
+        double host[kObsStage];
+        double* dev;
+    };
+    mutable std::mutex obs_mu;
+    mutable std::vector<std::unique_ptr<ObsSet>> obs_sets;
     ~carmpc_problem() {
         for (void* p : allocs) (void)hipFree(p);
+        for (auto& set : obs_sets) (void)hipFree(set->dev);
     }
     template <class T_>
     hipError_t alloc(T_** ptr, size_t count) {
@@ -482,6 +497,49 @@ int hetero_riccati_template(carmpc_hetero* h, const carmpc_hetero_desc* d) {
 }
 }  // namespace
 
+namespace {
+// Device copy of one set of observer constants, keyed by value.  The first use of a value set
+// uploads it with a blocking copy (a setup cost, like carmpc_problem_create); every later call
+// finds it and returns without touching the device, so the observer entry points only launch.
+int stage_observer(const carmpc_problem* P, int32_t ny, const double* C, const double* L, const double* Cd,
+                   const double* L2, const double* Bd, const double** dev) {
+    if (!P || !C || !L) return fail(CARMPC_EINVAL, "null argument");
+    if (!P->assembled) return fail(CARMPC_EINVAL, "observer needs an assembled problem (A, B)");
+    if (ny < 1 || ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
+    if ((Cd != nullptr) != (L2 != nullptr) || (Cd != nullptr) != (Bd != nullptr))
+        return fail(CARMPC_EINVAL, "Cd, L2 and Bd go together");
+    double host[carmpc_problem::kObsStage] = {};
+    std::memcpy(host, C, sizeof(double) * ny * NX);
+    std::memcpy(host + 8 * NX, L, sizeof(double) * NX * ny);
+    if (Cd) {
+        std::memcpy(host + 16 * NX, Cd, sizeof(double) * ny);
+        std::memcpy(host + 16 * NX + 8, L2, sizeof(double) * ny);
+        std::memcpy(host + 16 * NX + 16, Bd, sizeof(double) * NX);
+    }
+    std::lock_guard<std::mutex> lock(P->obs_mu);
+    for (const auto& set : P->obs_sets)
+        if (std::memcmp(set->host, host, sizeof(host)) == 0) {
+            *dev = set->dev;
+            return CARMPC_OK;
+        }
+    if (P->obs_sets.size() >= 64) return fail(CARMPC_ENOMEM, "more than 64 distinct observer constant sets on one problem");
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur), "hipGetDevice");
+    if (cur != P->device) return fail(CARMPC_EINVAL, "the problem belongs to another device than the current one");
+    auto set = std::make_unique<carmpc_problem::ObsSet>();
+    std::memcpy(set->host, host, sizeof(host));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&set->dev), sizeof(host)), "hipMalloc observer constants");
+    const hipError_t e = hipMemcpy(set->dev, host, sizeof(host), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(set->dev);
+        return hipfail(e, "upload observer constants");
+    }
+    *dev = set->dev;
+    P->obs_sets.push_back(std::move(set));
+    return CARMPC_OK;
+}
+}  // namespace
+
 extern "C" {
 
 const char* carmpc_last_error(void) { return g_err.c_str(); }
@@ -739,16 +797,7 @@ int carmpc_problem_get(const carmpc_problem* P, double* T, double* S, double* H,
 
 int carmpc_solve_batch(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref, double* u_out,
                        int32_t* status, int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
-    if (!P) return fail(CARMPC_EINVAL, "null problem");
-    if (batch < 0) return fail(CARMPC_EINVAL, "negative batch");
-    if (batch == 0) return CARMPC_OK;
-    if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
-    const Settings s = make_settings(settings);
-    int unsupported = 0;
-    hipError_t e = launch_solve(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
-    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
-    if (e != hipSuccess) return hipfail(e, "solve launch");
-    return CARMPC_OK;
+    return solve_batch_with_claim(P, batch, x0, xref, u_out, status, iters, settings, nullptr, stream);
 }
 
 int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, const int64_t* offsets,
@@ -778,7 +827,7 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
         if (!side) return hipfail(hipGetLastError(), "side streams");
         const size_t bytes = sizeof(unsigned) * kCounterStride * live;
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&counters), bytes, stream), "segment counters");
-        HIP_TRY(hipMemsetAsync(counters, 0, bytes, stream), "zero segment counters");
+        HIP_TRY(launch_zero_u32(counters, kCounterStride * live, stream), "zero segment counters");
         HIP_TRY(hipEventRecord(side->fork, stream), "fork event");
     }
     int k = 0, rc = CARMPC_OK;
@@ -1137,29 +1186,19 @@ int carmpc_closed_loop_batch(const carmpc_problem* P, int64_t batch, const carmp
     return CARMPC_OK;
 }
 
+int carmpc_problem_set_observer(const carmpc_problem* P, int32_t ny, const double* C, const double* L,
+                                const double* Cd, const double* L2, const double* Bd) {
+    const double* dev = nullptr;
+    return stage_observer(P, ny, C, L, Cd, L2, Bd, &dev);
+}
+
 int carmpc_observer_dist_batch(const carmpc_problem* P, int64_t batch, const double* y, int32_t ny, const double* C,
                                const double* L1, const double* Cd, const double* L2, const double* Bd, double* xhat,
                                double* dhat, const double* uprev, int64_t ld_uprev, hipStream_t stream) {
     if (!P || !y || !C || !L1 || !Cd || !L2 || !Bd || !xhat || !dhat || !uprev) return fail(CARMPC_EINVAL, "null argument");
-    if (!P->assembled) return fail(CARMPC_EINVAL, "observer needs an assembled problem (A, B)");
-    if (ny < 1 || ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
-    thread_local double* dCL = nullptr;
-    thread_local int dev_of = -1;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    constexpr int kStage = 2 * 8 * NX + 8 + 8 + NX;
-    if (!dCL || dev_of != dev) {
-        HIP_TRY(hipMalloc(&dCL, sizeof(double) * kStage), "hipMalloc observer");
-        dev_of = dev;
-    }
-    std::vector<double> host(kStage, 0.0);
-    std::memcpy(host.data(), C, sizeof(double) * ny * NX);
-    std::memcpy(host.data() + 8 * NX, L1, sizeof(double) * NX * ny);
-    std::memcpy(host.data() + 16 * NX, Cd, sizeof(double) * ny);
-    std::memcpy(host.data() + 16 * NX + 8, L2, sizeof(double) * ny);
-    std::memcpy(host.data() + 16 * NX + 16, Bd, sizeof(double) * NX);
-    HIP_TRY(hipMemcpyAsync(dCL, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice, stream), "copy observer");
-    HIP_TRY(hipStreamSynchronize(stream), "sync observer");
+    const double* dCL = nullptr;
+    const int rc = stage_observer(P, ny, C, L1, Cd, L2, Bd, &dCL);
+    if (rc != CARMPC_OK) return rc;
     ObsArgs a{};
     a.batch = batch; a.ny = ny; a.nu = P->dev.nu; a.ld_uprev = ld_uprev;
     a.A = P->dev.A; a.B = P->dev.B; a.C = dCL; a.L = dCL + 8 * NX; a.y = y; a.uprev = uprev; a.xhat = xhat;
@@ -1171,22 +1210,9 @@ int carmpc_observer_dist_batch(const carmpc_problem* P, int64_t batch, const dou
 int carmpc_observer_batch(const carmpc_problem* P, int64_t batch, const double* y, int32_t ny, const double* C,
                           const double* L, double* xhat, const double* uprev, int64_t ld_uprev, hipStream_t stream) {
     if (!P || !y || !C || !L || !xhat || !uprev) return fail(CARMPC_EINVAL, "null argument");
-    if (!P->assembled) return fail(CARMPC_EINVAL, "observer needs an assembled problem (A, B)");
-    if (ny < 1 || ny > 8) return fail(CARMPC_EUNSUPPORTED, "ny must be in [1,8]");
-    // C and L are tiny host arrays: stage them in a per-thread device cache.
-    thread_local double* dCL = nullptr;
-    thread_local int dev_of = -1;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    if (!dCL || dev_of != dev) {
-        HIP_TRY(hipMalloc(&dCL, sizeof(double) * 2 * 8 * NX), "hipMalloc observer");
-        dev_of = dev;
-    }
-    std::vector<double> host(2 * 8 * NX, 0.0);
-    std::memcpy(host.data(), C, sizeof(double) * ny * NX);
-    std::memcpy(host.data() + 8 * NX, L, sizeof(double) * NX * ny);
-    HIP_TRY(hipMemcpyAsync(dCL, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice, stream), "copy C,L");
-    HIP_TRY(hipStreamSynchronize(stream), "sync C,L");
+    const double* dCL = nullptr;
+    const int rc = stage_observer(P, ny, C, L, nullptr, nullptr, nullptr, &dCL);
+    if (rc != CARMPC_OK) return rc;
     ObsArgs a{};
     a.batch = batch; a.ny = ny; a.nu = P->dev.nu; a.ld_uprev = ld_uprev;
     a.A = P->dev.A; a.B = P->dev.B; a.C = dCL; a.L = dCL + 8 * NX; a.y = y; a.uprev = uprev; a.xhat = xhat;
@@ -1202,3 +1228,25 @@ int carmpc_plant_step_batch(int64_t batch, double* state, const double* u, int64
 }
 
 }  // extern "C"
+
+// carmpc_solve_batch with the claim counter supplied by the caller (already zeroed, stream-ordered
+// before the launch); claim == nullptr: a stream-ordered allocation per launch.
+namespace carmpc {
+int solve_batch_with_claim(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref, double* u_out,
+                           int32_t* status, int32_t* iters, const carmpc_settings* settings, unsigned* claim,
+                           hipStream_t stream) {
+    if (!P) return fail(CARMPC_EINVAL, "null problem");
+    if (batch < 0) return fail(CARMPC_EINVAL, "negative batch");
+    if (batch == 0) return CARMPC_OK;
+    if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
+    Settings s = make_settings(settings);
+    s.claim = claim;
+    int unsupported = 0;
+    hipError_t e = launch_solve(P->dev, batch, x0, xref, u_out, P->dev.n, status, iters, s, stream, &unsupported);
+    if (unsupported) return fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+    if (e != hipSuccess) return hipfail(e, "solve launch");
+    return CARMPC_OK;
+}
+int problem_device(const carmpc_problem* P) { return P ? P->device : -1; }
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace carmpc

@@ -91,6 +91,21 @@ struct DevProblem {
     const double *het_A, *het_B, *het_P;                    // B x 16, B x 8, B x 16
 };
 
+// CarSimulator.check_input with clip=False (simulator.py:88-95) asserts
+//   [a, -a] <= [acc_upper, -acc_lower]   and   [delta, -delta] <= [delta_upper, -delta_lower]
+// on Python lists, whose order is lexicographic: the second pair is only compared when the
+// first elements are equal.  So an input is rejected when it exceeds the UPPER limit only
+// (2 + 0.05, pi/4 + 0.05, simulator.py:44-45); large negative inputs pass.  NaN is rejected
+// (NaN != hi, then NaN <= hi is false).
+__host__ __device__ inline bool list_le2(double a0, double a1, double b0, double b1) {
+    return a0 < b0 || (a0 == b0 && a1 <= b1);
+}
+__host__ __device__ inline bool input_rejected(double acc, double delta) {
+    const double acc_hi = 2.0 + 0.05, acc_lo = -2.0 - 0.05;
+    const double del_hi = 3.14159265358979323846 / 4 + 0.05, del_lo = -3.14159265358979323846 / 4 - 0.05;
+    return !list_le2(acc, -acc, acc_hi, -acc_lo) || !list_le2(delta, -delta, del_hi, -del_lo);
+}
+
 struct Settings {
     double tol, tol_mu;
     int32_t max_iter;
@@ -111,13 +126,16 @@ __device__ __forceinline__ int64_t wave_claim(unsigned* c) {
     if ((threadIdx.x & 63) == 0) v = atomicAdd(c, 1u);
     return (int64_t)__builtin_amdgcn_readfirstlane(v);
 }
+// Clear n 32-bit words with a small kernel (not hipMemsetAsync, so that a caller may record
+// the launch sequence into a HIP graph).
+hipError_t launch_zero_u32(unsigned* ptr, int n, hipStream_t stream);
 template <class Launch>
 inline hipError_t launch_with_claim(Settings s, int64_t batch, hipStream_t stream, Launch&& launch) {
     unsigned* counter = nullptr;
     hipError_t e = hipSuccess;
     if (batch > 1 && !s.claim) {
         if ((e = hipMallocAsync(reinterpret_cast<void**>(&counter), sizeof(unsigned), stream)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(counter, 0, sizeof(unsigned), stream)) != hipSuccess) return e;
+        if ((e = launch_zero_u32(counter, 1, stream)) != hipSuccess) return e;
         s.claim = counter;
     }
     e = launch(s);
@@ -127,6 +145,13 @@ inline hipError_t launch_with_claim(Settings s, int64_t batch, hipStream_t strea
     }
     return e;
 }
+
+// capi.hip internals shared with the other translation units of the C ABI.
+int solve_batch_with_claim(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref, double* u_out,
+                           int32_t* status, int32_t* iters, const carmpc_settings* settings, unsigned* claim,
+                           hipStream_t stream);
+int problem_device(const carmpc_problem* P);
+int set_error(int code, const char* msg);   // records the calling thread's last-error message, returns code
 
 // Argument blocks of the setup kernels (assembly.hip).
 struct AsmArgs {

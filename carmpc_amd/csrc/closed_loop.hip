@@ -17,12 +17,6 @@ namespace carmpc {
 
 namespace {
 
-__device__ __forceinline__ bool input_bad(double acc, double delta) {
-    // CarSimulator.check_input with clip=False asserts these bounds (simulator.py:45-46,83-97)
-    const double acc_hi = 2.0 + 0.05, del_hi = M_PI / 4 + 0.05;
-    return acc > acc_hi || -acc > acc_hi || delta > del_hi || -delta > del_hi;
-}
-
 __global__ void loop_advance_kernel(LoopArgs a, int32_t i) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (slot == 0) *a.cnt_next = 0;   // the other list is rebuilt by loop_finish_kernel
@@ -30,7 +24,7 @@ __global__ void loop_advance_kernel(LoopArgs a, int32_t i) {
     const int64_t b = a.idx_cur[slot];
     double* st = a.state + b * NX;
     const double acc = a.u[b * a.ld_u + 0], delta = a.u[b * a.ld_u + 1];
-    if (input_bad(acc, delta)) {
+    if (input_rejected(acc, delta)) {   // check_input, clip=False (simulator.py:83-97)
         a.outcome[b] = CARMPC_LOOP_INPUT_VIOLATION;   // the runner stops at the assertion, before the step
         a.steps[b] = i;
         return;

@@ -76,9 +76,13 @@ class CarSimulator:
         a, delta_f = control_input
         if self.clip:
             return np.clip(control_input, [self.acc_lower, self.delta_lower], [self.acc_upper, self.delta_upper])
-        if not (a <= self.acc_upper and -a <= -self.acc_lower):
+        # The reference compares Python lists, [a, -a] <= [acc_upper, -acc_lower]
+        # (simulator.py:92-95): list order is lexicographic, so the lower limit is only looked at
+        # when a == acc_upper, and inputs below it pass.  Kept as is: callers see the same
+        # AssertionError for the same inputs.
+        if not ([a, -a] <= [self.acc_upper, -self.acc_lower]):
             raise AssertionError(f"Acceleration should be between [{self.acc_lower, self.acc_upper}], but is {a}.")
-        if not (delta_f <= self.delta_upper and -delta_f <= -self.delta_lower):
+        if not ([delta_f, -delta_f] <= [self.delta_upper, -self.delta_lower]):
             raise AssertionError(f"Steering angle should be between [{self.delta_lower:.3f}, "
                                  f"{self.delta_upper:.3f}], but is {delta_f}.")
         return control_input

@@ -157,16 +157,26 @@ int carmpc_solve_batch_dist(const carmpc_problem* prob, int64_t batch, const dou
                             const carmpc_settings* settings, hipStream_t stream);
 /* Disturbance-augmented Luenberger observer (mpc.py:598-612), in place on device:
  * e = y - C xhat - Cd dhat; xhat <- A xhat + Bd dhat + B uprev + L1 e; dhat <- dhat + L2 . e.
- * C (ny x NX), L1 (NX x ny), Cd, L2 (ny), Bd (NX) are host arrays. */
+ * C (ny x NX), L1 (NX x ny), Cd, L2 (ny), Bd (NX) are host arrays, compared by value with the
+ * sets already staged on the problem (carmpc_problem_set_observer). */
 int carmpc_observer_dist_batch(const carmpc_problem* prob, int64_t batch, const double* y, int32_t ny,
                                const double* C, const double* L1, const double* Cd, const double* L2,
                                const double* Bd, double* xhat, double* dhat, const double* uprev,
                                int64_t ld_uprev, hipStream_t stream);
 
+/* Stage a set of observer constants on the device ahead of time (MPCOutputFB.__init__ sets C
+ * and L once, mpc.py:387-404; MPCOutputFBWithDisturbance Bd, Cd, L1, L2, mpc.py:530-546).  The
+ * observer entry points do this themselves on the first call with a given set of values; calls
+ * with values already staged only launch the kernel (no copy, no host synchronisation).
+ * Cd, L2, Bd may all be NULL (plain Luenberger observer).  Blocking; at most 64 distinct sets. */
+int carmpc_problem_set_observer(const carmpc_problem* prob, int32_t ny, const double* C, const double* L,
+                                const double* Cd, const double* L2, const double* Bd);
+
 /* Luenberger observer (mpc.py:439-448), in place on device:
  *   xhat <- A xhat + B uprev + L (y - C xhat)
  * y B*ny, xhat B*nx, uprev rows at stride ld_uprev (first nu entries used),
- * C ny*nx, L nx*ny host arrays.  A, B come from the problem. */
+ * C ny*nx, L nx*ny host arrays (staged on the device at their first use, see
+ * carmpc_problem_set_observer).  A, B come from the problem. */
 int carmpc_observer_batch(const carmpc_problem* prob, int64_t batch, const double* y, int32_t ny,
                           const double* C, const double* L, double* xhat, const double* uprev,
                           int64_t ld_uprev, hipStream_t stream);

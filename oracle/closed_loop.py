@@ -21,12 +21,17 @@ from . import assembly as oa
 from . import qp as oq
 
 REACHED, INFEASIBLE, INPUT_VIOLATION, TIMEOUT, SOLVER_FAILURE = 0, 1, 2, 3, 4
-ACC_HI, DEL_HI = 2.0 + 0.05, np.pi / 4 + 0.05      # simulator.py:45-46
+ACC_LO, ACC_HI = -2 - 0.05, 2 + 0.05                        # simulator.py:45
+DEL_LO, DEL_HI = -np.pi / 4 - 0.05, np.pi / 4 + 0.05        # simulator.py:44
 
 
 def input_bad(u) -> bool:
-    a, delta = u[0], u[1]
-    return bool(a > ACC_HI or -a > ACC_HI or delta > DEL_HI or -delta > DEL_HI)
+    """check_input with clip=False (simulator.py:88-95).  The reference compares Python LISTS,
+    ``[a, -a] <= [acc_upper, -acc_lower]``: list order is lexicographic, so the second pair only
+    counts when ``a == acc_upper`` -- inputs below the lower limit pass.  Restated with the same
+    list comparison."""
+    a, delta = float(u[0]), float(u[1])
+    return not ([a, -a] <= [ACC_HI, -ACC_LO] and [delta, -delta] <= [DEL_HI, -DEL_LO])
 
 
 def run(asm, start, mode=0, last_step=151, goal_tol=0.1, steps_update=1, dt=oa.DT_SIMULATION, xref=None,

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 X_TOL = 1e-6
 
 
-def _controller(kind, start=(5.0, -1.5, 0.0, 0.0), kernel=0):
+def _controller(kind, start=(5.0, -1.5, 0.0, 0.0), kernel=0, **flags):
     from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE, N
     from carmpc_amd.environments import ENVIRONMENTS
     from carmpc_amd.qp import SolverSettings
@@ -23,7 +23,7 @@ def _controller(kind, start=(5.0, -1.5, 0.0, 0.0), kernel=0):
     env = ENVIRONMENTS["RoadMultipleCarsEnv"]()
     if kind == 0:
         c = MPCStateFB(dt=DT_CONTROL, N=N, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT, env=env,
-                       terminal_set_dir=TERMINAL_SETS)
+                       terminal_set_dir=TERMINAL_SETS, **flags)
     elif kind == 1:
         c = MPCOutputFB(dt=DT_CONTROL, N=N, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT,
                         init_state=list(start), env=env, terminal_set_dir=TERMINAL_SETS)
@@ -70,6 +70,37 @@ def test_state_feedback_loop(gpu_available, kernel):
     assert refs[0]["outcome"] == ocl.REACHED and refs[0]["steps"] == 52   # the example's start
     outcomes = {r["outcome"] for r in refs}
     assert ocl.REACHED in outcomes and ocl.INFEASIBLE in outcomes
+    _compare(res, refs)
+
+
+def test_state_feedback_loop_without_input_constraint(gpu_available):
+    """input_constraint=False: the QP's inputs leave the actuator range.  The reference's
+    check_input compares Python lists (simulator.py:92-95), so only inputs ABOVE the upper
+    limits stop a run; hard braking below -2.05 m/s^2 keeps driving."""
+    from carmpc_amd.closed_loop import run_closed_loop
+    from oracle import assembly as oa
+    from oracle import closed_loop as ocl
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS, input_constraint_on=False)
+    rng = np.random.default_rng(21)
+    n = 24
+    starts = np.column_stack([rng.uniform(0, 29, n), rng.uniform(-2.8, 2.8, n), rng.uniform(-0.3, 0.3, n),
+                              rng.uniform(0, 5, n)])
+    starts = np.vstack([[27.0, 1.0, 0.0, 4.5], [29.0, 1.5, 0.0, 4.0], [5.0, -1.5, 0.0, 0.0], starts])
+    base = ocl.c_solver(asm, threads=8)
+    refs, braked = [], []
+    for s0 in starts:
+        amin = [0.0]
+
+        def solve(x0, xr, d):
+            st, u = base(x0, xr, d)
+            if st == 0:
+                amin[0] = min(amin[0], u[0])
+            return st, u
+        refs.append(ocl.run(asm, s0, mode=0, last_step=151, goal_tol=0.1, solve=solve))
+        braked.append(amin[0] < -2.05 and refs[-1]["steps"] > 2)
+    assert any(braked)                                              # ran on after an input below the range
+    assert any(r["outcome"] == ocl.INPUT_VIOLATION for r in refs)   # stopped by one above it
+    res = run_closed_loop(_controller(0, input_constraint=False), starts)
     _compare(res, refs)
 
 

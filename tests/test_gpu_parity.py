@@ -53,9 +53,36 @@ def test_assembly_kernel_matches_oracle(gpu_available, name, N):
     np.testing.assert_allclose(m["G"], asm.G, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(m["E"], asm.E, rtol=1e-12, atol=1e-12)
     np.testing.assert_array_equal(m["w0"], asm.w0)
-    golden = np.load(f"{GOLDEN}/assembly_{name}_N{N}.npz")
-    np.testing.assert_allclose(m["H"], golden["H"], rtol=1e-12, atol=1e-10)
-    np.testing.assert_allclose(m["S"], golden["S"], rtol=0, atol=1e-13)
+    # ... and against the dump of the reference's own constructor (lib/mpc.py:22-117) and
+    # constraint builders (mpc.py:196-253): its stacks composed with its T and S
+    g = np.load(f"{GOLDEN}/assembly_{name}_N{N}.npz")
+    np.testing.assert_allclose(m["T"], g["T"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(m["S"], g["S"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(m["H"], g["H"], rtol=1e-12, atol=1e-10)
+    np.testing.assert_allclose(m["h"], g["h"], rtol=1e-12, atol=1e-10)
+    A_all = np.vstack((g["term_A"], g["state_A"]))
+    np.testing.assert_allclose(m["G"], A_all @ g["S"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(m["E"], A_all @ g["T"], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(m["w0"], np.hstack((g["term_b"], g["state_b"])))
+
+
+def test_assembly_kernel_fallback_matches_reference(gpu_available, tmp_path):
+    """Goal-box terminal rows of the reference constructor when no terminal-set file exists
+    (mpc.py:107-117), from its own dump."""
+    import json
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    g = np.load(f"{GOLDEN}/assembly_fallback_RoadEnv_N10.npz")
+    goal = json.load(open(f"{GOLDEN}/meta.json"))["fallback_goal"]
+    asm = oa.build("RoadEnv", 10, terminal_set_dir=str(tmp_path), goal=goal)
+    qp = QPProblem(N=10, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    m = qp.matrices()
+    A_all = np.vstack((g["term_A"], g["state_A"]))
+    np.testing.assert_allclose(m["G"], A_all @ g["S"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(m["E"], A_all @ g["T"], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(m["w0"], np.hstack((g["term_b"], g["state_b"])))
 
 
 KERNELS = [1, 2, 4, 5, 6, 7]   # carmpc_settings.kernel: dense; staged; staged A/B variants; riccati (default)
@@ -201,8 +228,26 @@ def test_observer_and_plant_kernels(gpu_available):
     qp.observe(torch.as_tensor(y).cuda(), xt, torch.as_tensor(up).cuda(), oa.C_OUT, oa.L_OBS)
     ref = np.stack([oa.luenberger_observer(asm.A, asm.B, xh[i], up[i], y[i]) for i in range(B)])
     np.testing.assert_allclose(xt.cpu().numpy(), ref, rtol=1e-14, atol=1e-13)
+    # the reference's own observer methods on seeded tuples (mpc.py:439-448, 598-612)
+    o = np.load(f"{GOLDEN}/observer.npz")
+    xt = torch.as_tensor(o["x_estimate"].copy()).cuda()
+    qp.observe(torch.as_tensor(o["y0"]).cuda(), xt, torch.as_tensor(o["previous_u"]).cuda(), o["C"], o["L"])
+    np.testing.assert_allclose(xt.cpu().numpy(), o["next"], rtol=0, atol=1e-13)
+    xt = torch.as_tensor(o["x_estimate"].copy()).cuda()
+    dt_ = torch.as_tensor(o["d_estimate"].copy()).cuda()
+    qp.observe_dist(torch.as_tensor(o["y0"]).cuda(), xt, dt_, torch.as_tensor(o["previous_u"]).cuda(), o["C"], o["L1"],
+                    o["Cd"], o["L2"], o["Bd"])
+    np.testing.assert_allclose(xt.cpu().numpy(), o["next_dist_x"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(dt_.cpu().numpy(), o["next_dist_d"], rtol=0, atol=1e-13)
     g = np.load(f"{GOLDEN}/plant.npz")
     st = torch.as_tensor(g["state"].copy()).cuda()
     bad = plant_step(st, torch.as_tensor(g["u"]).cuda(), 0.2, 3.5)
     np.testing.assert_allclose(st.cpu().numpy(), g["next"], rtol=1e-14, atol=1e-13)
     assert int(bad.sum()) == 0
+    # inputs outside the limits: flags == where the reference's check_input raised
+    # (simulator.py:92-95, a list comparison: only the upper limits reject); rows are stepped anyway
+    st = torch.as_tensor(g["oob_state"].copy()).cuda()
+    bad = plant_step(st, torch.as_tensor(g["oob_u"]).cuda(), 0.2, 3.5)
+    np.testing.assert_array_equal(bad.cpu().numpy(), g["oob_raised"])
+    keep = g["oob_raised"] == 0
+    np.testing.assert_allclose(st.cpu().numpy()[keep], g["oob_next"][keep], rtol=1e-14, atol=1e-13)

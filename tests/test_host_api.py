@@ -24,6 +24,38 @@ def _ctrl(name, N, cls="MPCStateFB", **kw):
 
 
 @pytest.mark.parametrize("name,N", CONFIGS)
+def test_constructor_matches_reference_constructor(name, N):
+    """Host mirror of MPC.__init__ against the dump of the reference's own constructor and
+    constraint builders (tests/golden/assembly_*.npz, tools/make_golden.py)."""
+    c = _ctrl(name, N)
+    g = np.load(os.path.join(GOLDEN, f"assembly_{name}_N{N}.npz"))
+    np.testing.assert_array_equal(c.A, g["A"])
+    np.testing.assert_array_equal(c.B, g["B"])
+    np.testing.assert_allclose(c.P, g["P"], rtol=1e-13, atol=0)
+    np.testing.assert_allclose(c.K, g["K"], rtol=1e-12, atol=1e-14)
+    np.testing.assert_array_equal(c.goal, g["goal"])
+    np.testing.assert_array_equal(c.input_upper, g["input_upper"])
+    np.testing.assert_array_equal(c.input_lower, g["input_lower"])
+    for fn, key in ((c.terminal_constraint, "term"), (c.input_constraint, "input"), (c.state_constraint, "state")):
+        A, b = fn()
+        np.testing.assert_array_equal(A, g[key + "_A"])
+        np.testing.assert_array_equal(b, g[key + "_b"])
+
+
+def test_constructor_fallback_matches_reference(tmp_path):
+    from carmpc_amd import environments, mpc
+    meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
+    g = np.load(os.path.join(GOLDEN, "assembly_fallback_RoadEnv_N10.npz"))
+    env = environments.RoadEnv()
+    env.goal = list(meta["fallback_goal"])
+    c = mpc.MPCStateFB(0.2, 10, [0, 0, 0, 3], [0, 0], env=env, terminal_set_dir=str(tmp_path))
+    A, b = c.terminal_constraint()
+    np.testing.assert_array_equal(A, g["term_A"])
+    np.testing.assert_array_equal(b, g["term_b"])
+    np.testing.assert_array_equal(c.goal, g["goal"])
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
 def test_constructor_matches_oracle(name, N):
     c = _ctrl(name, N)
     asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
@@ -64,6 +96,12 @@ def test_output_fb_target_and_observer_host_forms():
     np.testing.assert_allclose(c.luenberger_observer(y), ref, rtol=1e-15)
     np.testing.assert_array_equal(c.C, oa.C_OUT)
     np.testing.assert_array_equal(c.L, oa.L_OBS)
+    # the reference's own method on seeded tuples (mpc.py:439-448)
+    g = np.load(os.path.join(GOLDEN, "observer.npz"))
+    np.testing.assert_array_equal(c.y_goal, g["y_goal"])
+    for i in range(len(g["y0"])):
+        c.x_estimate, c.previous_u = g["x_estimate"][i].copy(), g["previous_u"][i].copy()
+        np.testing.assert_allclose(c.luenberger_observer(g["y0"][i]), g["next"][i], rtol=0, atol=1e-13)
 
 
 def test_lqr_path():
@@ -80,8 +118,8 @@ def test_matrix_gen_mirror_matches_reference_outputs():
     for name, N in CONFIGS:
         g = np.load(os.path.join(GOLDEN, f"assembly_{name}_N{N}.npz"))
         T, S = mg.predmod(g["A"], g["B"], N)
-        np.testing.assert_allclose(T, g["T"], rtol=0, atol=1e-15)
-        np.testing.assert_allclose(S, g["S"], rtol=0, atol=1e-15)
+        np.testing.assert_allclose(T, g["T"], rtol=0, atol=1e-13)   # powers of A by a different product order
+        np.testing.assert_allclose(S, g["S"], rtol=0, atol=1e-13)
         H, h, const = mg.costgen(oa.STAGE_COST_Q, oa.STAGE_COST_R, g["P"], T, S, 4)
         np.testing.assert_allclose(H, g["H"], rtol=1e-13, atol=1e-10)
         np.testing.assert_allclose(h, g["h"], rtol=1e-13, atol=1e-10)
@@ -102,6 +140,17 @@ def test_simulator_mirror_matches_reference():
         sim.step([2.1, 0.0])                               # simulator.py:92-93
     with pytest.raises(AssertionError):
         sim.step([0.0, 1.0])
+    # outside the limits: same outcome as the reference's check_input, whose list comparison
+    # (simulator.py:92-95) only rejects inputs above the upper limits
+    for s0, u, raised, nxt in zip(g["oob_state"], g["oob_u"], g["oob_raised"], g["oob_next"]):
+        sim = CarSimulator(dt=0.2)
+        sim.reset(np.array(s0))
+        if raised:
+            with pytest.raises(AssertionError):
+                sim.step(u)
+        else:
+            sim.step(u)
+        np.testing.assert_array_equal(sim.state, nxt)
     clipped = CarSimulator(dt=0.2, clip=True).check_input([5.0, -2.0])
     np.testing.assert_allclose(clipped, [2.05, -np.pi / 4 - 0.05])
 

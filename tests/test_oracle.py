@@ -1,10 +1,14 @@
 """The oracle against the golden vectors produced from the reference (CPU only).
 
 Pins (see tests/golden/meta.json, tools/make_golden.py):
-  * assembly (T, S, H, h) == outputs of the reference's lib/matrix_gen.py;
+  * constructor (A, B, P, K, T, S, H, h, terminal rows, constraint stacks) == what the
+    reference's own lib/mpc.py::MPCStateFB.__init__ and its terminal_constraint() /
+    input_constraint() / state_constraint() produce, including the missing-file fallback;
+  * observers == the reference's own luenberger_observer methods on seeded tuples;
   * environments / configuration == the reference's objects and constants;
   * terminal-set data == the reference's terminal_sets/*.npy;
-  * plant == the reference's lib/simulator.CarSimulator on seeded pairs;
+  * plant == the reference's lib/simulator.CarSimulator on seeded pairs, and its check_input
+    outcome (raised / not raised) on inputs outside the limits;
   * QP solutions: KKT-certified optimum (parity vs cvxpy itself is unpinned: absent).
 """
 import json
@@ -24,25 +28,81 @@ def _meta():
         return json.load(f)
 
 
-@pytest.mark.parametrize("name,N", CONFIGS)
-def test_assembly_matches_reference_matrix_gen(name, N):
-    g = np.load(os.path.join(GOLDEN, f"assembly_{name}_N{N}.npz"))
-    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+def _check_against_reference_constructor(asm, g):
+    """asm (oracle restatement) against a dump of the reference's constructor and builders."""
+    N = asm.N
     np.testing.assert_array_equal(asm.A, g["A"])
     np.testing.assert_array_equal(asm.B, g["B"])
+    np.testing.assert_allclose(asm.P, g["P"], rtol=1e-13, atol=0)     # same LAPACK call (mpc.py:70)
+    np.testing.assert_allclose(asm.K, g["K"], rtol=1e-12, atol=1e-14)
     np.testing.assert_allclose(asm.T, g["T"], rtol=0, atol=1e-14)   # BLAS rounding only
     np.testing.assert_allclose(asm.S, g["S"], rtol=0, atol=1e-14)
     np.testing.assert_allclose(asm.H, g["H"], rtol=1e-14, atol=1e-11)
     np.testing.assert_allclose(asm.h, g["h"], rtol=1e-14, atol=1e-11)
+    np.testing.assert_array_equal(asm.goal, g["goal"])
+    np.testing.assert_array_equal(asm.input_upper, g["input_upper"])
+    np.testing.assert_array_equal(asm.input_lower, g["input_lower"])
+    # the three stacks, exactly as the reference's builders return them (mpc.py:196-253)
+    np.testing.assert_array_equal(asm.term_A, g["term_A"])
+    np.testing.assert_array_equal(asm.term_b, g["term_b"])
+    iA, ib = oa.input_constraint(N, 2, asm.input_upper, asm.input_lower)
+    np.testing.assert_array_equal(iA, g["input_A"])
+    np.testing.assert_array_equal(ib, g["input_b"])
+    sA, sb = oa.state_constraint(N, 4, asm.state_rows_A, asm.state_rows_b)
+    np.testing.assert_array_equal(sA, g["state_A"])
+    np.testing.assert_array_equal(sb, g["state_b"])
+    # condensed rows G u <= w0 - E x0: the reference's stacks composed with ITS T and S
+    # (x = T x0 + S u, mpc.py:319; order terminal, then state: mpc.py:323-332)
+    A_all = np.vstack((g["term_A"], g["state_A"]))
+    np.testing.assert_allclose(asm.G, A_all @ g["S"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(asm.E, A_all @ g["T"], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(asm.w0, np.hstack((g["term_b"], g["state_b"])))
+    np.testing.assert_array_equal(asm.ub, g["input_b"][:2 * N])
+    np.testing.assert_array_equal(asm.lb, -g["input_b"][2 * N:])
+
+
+@pytest.mark.parametrize("name,N", CONFIGS)
+def test_assembly_matches_reference_constructor(name, N):
+    g = np.load(os.path.join(GOLDEN, f"assembly_{name}_N{N}.npz"))
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+    _check_against_reference_constructor(asm, g)
     np.testing.assert_array_equal(asm.term_A[:, -4:], g["term"][:, :4])
     np.testing.assert_array_equal(asm.term_b, g["term"][:, 4])
-    # DARE fixed point (mpc.py:70) and LQR gain (mpc.py:81)
+    # DARE fixed point (mpc.py:70)
     A, B, P, Q, R = asm.A, asm.B, asm.P, oa.STAGE_COST_Q, oa.STAGE_COST_R
     res = A.T @ P @ A - P - A.T @ P @ B @ np.linalg.solve(R + B.T @ P @ B, B.T @ P @ A) + Q
     assert np.abs(res).max() < 1e-9
-    np.testing.assert_allclose(asm.K, g["K"], rtol=1e-12)
-    # survey §8a a3 spot values
     assert abs(P[0, 0] - 60.13) < 5e-3 and abs(P[2, 2] - 843.30) < 5e-3
+
+
+def test_fallback_matches_reference_constructor(tmp_path):
+    """No terminal-set file for the goal -> the reference's goal box (mpc.py:107-117)."""
+    g = np.load(os.path.join(GOLDEN, "assembly_fallback_RoadEnv_N10.npz"))
+    goal = _meta()["fallback_goal"]
+    asm = oa.build("RoadEnv", 10, terminal_set_dir=str(tmp_path), goal=goal)
+    assert asm.term_file is None and g["term_A"].shape == (8, 44)
+    _check_against_reference_constructor(asm, g)
+
+
+def test_observer_restatements_match_reference_methods():
+    """oracle luenberger_observer / disturbance_observer against the reference's own methods
+    (mpc.py:439-448, 598-612) and their constants (mpc.py:387-404, 530-546)."""
+    g = np.load(os.path.join(GOLDEN, "observer.npz"))
+    np.testing.assert_array_equal(oa.C_OUT, g["C"])
+    np.testing.assert_array_equal(oa.L_OBS, g["L"])
+    np.testing.assert_array_equal(oa.BD_DIST, g["Bd"])
+    np.testing.assert_array_equal(oa.CD_DIST, g["Cd"])
+    np.testing.assert_array_equal(oa.L1_DIST, g["L1"])
+    np.testing.assert_array_equal(oa.L2_DIST, g["L2"])
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    np.testing.assert_array_equal(oa.C_OUT @ asm.goal, g["y_goal"])
+    for i in range(len(g["y0"])):
+        x = oa.luenberger_observer(asm.A, asm.B, g["x_estimate"][i], g["previous_u"][i], g["y0"][i])
+        np.testing.assert_allclose(x, g["next"][i], rtol=0, atol=1e-13)
+        xd, dd = oa.disturbance_observer(asm.A, asm.B, g["x_estimate"][i], g["d_estimate"][i], g["previous_u"][i],
+                                         g["y0"][i])
+        np.testing.assert_allclose(xd, g["next_dist_x"][i], rtol=0, atol=1e-13)
+        np.testing.assert_allclose(dd, g["next_dist_d"][i], rtol=0, atol=1e-13)
 
 
 def test_environment_and_configuration_data():
@@ -125,9 +185,18 @@ def test_c_oracle_status_against_lp_ground_truth():
 
 
 def test_plant_restatement_matches_reference_simulator():
+    from oracle import closed_loop as ocl
     g = np.load(os.path.join(GOLDEN, "plant.npz"))
     for s, u, nxt in zip(g["state"], g["u"], g["next"]):
         np.testing.assert_allclose(oa.plant_step(s, u), nxt, rtol=0, atol=1e-14)
+        assert not ocl.input_bad(u)
+    # inputs outside the limits: the reference's check_input compares lists lexicographically
+    # (simulator.py:92-95), so only inputs above the UPPER limits raise
+    assert g["oob_raised"].sum() == 10 and len(g["oob_raised"]) == 30
+    for s, u, raised, nxt in zip(g["oob_state"], g["oob_u"], g["oob_raised"], g["oob_next"]):
+        assert ocl.input_bad(u) == bool(raised), u
+        if not raised:
+            np.testing.assert_allclose(oa.plant_step(s, u), nxt, rtol=0, atol=1e-14)
 
 
 def test_closed_loop_statefb_reproduces_golden_trace():
