@@ -27,7 +27,7 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
            "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
            "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
-           "carmpc_hetero_get", "carmpc_set_serial_segments",
+           "carmpc_hetero_get", "carmpc_set_serial_segments", "carmpc_solve_batch_noalloc",
            "carmpc_problem_set_observer")
 
 # outcomes of carmpc_closed_loop_batch (carmpc.h)
@@ -96,6 +96,7 @@ def load():
         "carmpc_problem_info": ([vp, ip, ip, ip, ip, ip], ctypes.c_int),
         "carmpc_problem_get": ([vp, dp, dp, dp, dp, dp, dp, dp, ip], ctypes.c_int),
         "carmpc_solve_batch": ([vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
+        "carmpc_solve_batch_noalloc": ([vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_problem_set_observer": ([vp, i32, dp, dp, dp, dp, dp], ctypes.c_int),
         "carmpc_solve_segments": ([ctypes.POINTER(vp), i32, ctypes.POINTER(i64), vp, vp, vp, i64, vp, vp,
                                    ctypes.POINTER(Settings), vp], ctypes.c_int),

@@ -12,7 +12,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libcarmpc.so")
-SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip"]
+SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip", "noalloc.hip"]
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
 # -packed-fp32-ops off: hipcc -O3 forms v_pk_*_f32 from ordinary float code by itself and some of
 # their forms have given wrong results on these GPUs; the flag only concerns the device pass (the

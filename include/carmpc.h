@@ -135,6 +135,20 @@ int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* 
                        double* u_out, int32_t* status, int32_t* iters,
                        const carmpc_settings* settings, hipStream_t stream);
 
+/* carmpc_solve_batch for callers that cannot allocate: code under HIP graph capture, tight
+ * serving loops, harnesses that forbid hipMalloc.  It has no counterpart in the reference.  Same
+ * arguments, results and kernels as carmpc_solve_batch; the kernels' claim counter (the only
+ * device memory the solve uses beyond its inputs and outputs) lives in a 256-byte static device
+ * array of the library instead of a stream-ordered allocation, and the call makes no hipMalloc,
+ * hipFree or other allocating call.  batch <= CARMPC_NOALLOC_MAX_BATCH, else CARMPC_EUNSUPPORTED.
+ * All calls on one GPU share that array: the counter is cleared at the start of each call (on
+ * `stream`), and two calls whose kernels overlap on one GPU -- from different streams or threads --
+ * race on it.  Call it with the problem's device current. */
+#define CARMPC_NOALLOC_MAX_BATCH ((int64_t)1 << 30)
+int carmpc_solve_batch_noalloc(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
+                               double* u_out, int32_t* status, int32_t* iters,
+                               const carmpc_settings* settings, hipStream_t stream);
+
 /* Several problems in one call: instances grouped by problem, segment j is
  * [offsets[j], offsets[j+1]) (host array of nprobs+1).  Row strides follow
  * each problem's n; u_out uses a common row stride ld_u >= max n.  The segments' launches are
