@@ -1,24 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: batched MPC QP solves/s on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[4], weak-scaled): every rank solves a shard of
-131,072 mixed Road*/Env instances (RoadEnv / RoadOneCarEnv / RoadMultipleCarsEnv,
-N=20, n=40, fp64), grouped by environment; at 8 GPUs that is the 1,048,576-instance
-config.  One timed step = one pass of the hot path (device QP solve of the whole
-shard, inputs resident in HBM).  The shard split needs no collective; the only
-communication is the max-over-ranks of the timing.
+Default workload (BASELINE.json configs[4], weak-scaled): every rank solves a shard of 131,072
+mixed Road*/Env instances (RoadEnv / RoadOneCarEnv / RoadMultipleCarsEnv, N = 20, n = 40, fp64),
+grouped by environment; at 8 GPUs that is the 1,048,576-instance configuration.  One timed step =
+one pass of the hot path over the shard (inputs resident in HBM).  The shard split needs no
+collective; the only communication is the barrier and the max-over-ranks of the wall time, both
+over gloo on host memory.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config5|config4|config3|config2]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.
+``--backend cpu`` runs the same control flow on the library's CPU QP path (hosts without a GPU;
+the distributed flow is tested this way under gloo).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 
@@ -29,255 +29,441 @@ sys.path.insert(0, REPO)
 
 ENVS = ("RoadEnv", "RoadOneCarEnv", "RoadMultipleCarsEnv")
 PER_GPU = 131072
-N_HOR = 20
-FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 dense (vector == matrix), spec
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64, vector FMA rate == matrix (MFMA) rate, vendor figure
 HBM_PEAK_GBS = 8000.0
+METRIC = "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X"
+
+# workload -> (environments, horizon, default per-GPU batch, controller, description)
+WORKLOADS = {
+    "config5": (ENVS, 20, PER_GPU, "statefb", "config5_mixed_road_envs_N20_weak"),
+    "config4": (("RoadMultipleCarsEnv",), 20, 65536, "outputfb", "config4_RoadMultipleCarsEnv_outputfb_N20"),
+    "config3": (("RoadOneCarEnv",), 20, 65536, "statefb", "config3_RoadOneCarEnv_statefb_N20"),
+    "config2": (("RoadEnv",), 10, 4096, "statefb", "config2_RoadEnv_statefb_N10"),
+}
+KNAME = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 7: "ipm_riccati"}
+KDESC = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
+         2: "ipm_staged (wavefront per QP, stage-structured G/H products and Riccati-style M build)",
+         3: "ipm_dense, 4 waves per workgroup",
+         7: "ipm_riccati (16 lanes per QP, 4 QPs per wavefront, row state in registers, stage-form Riccati "
+            "factorization and solves, per-group instance refill)"}
 
 
-def sample_shard(rank: int, B: int, goals):
-    """Config 5 inputs: env_id ~ U{0,1,2}, x in [g_x-25, g_x], y in [-3,3],
-    psi in [-pi/8, pi/8], v in [-1, 5]; grouped by env (sorted)."""
-    rng = np.random.default_rng(5 * 1000 + rank)
-    env = np.sort(rng.integers(0, len(ENVS), B))
+def sample_shard(rank: int, B: int, goals, seed: int = 5):
+    """Config-5 inputs: env_id ~ U{0..len(goals)-1}, x in [g_x - 25, g_x], y in [-3, 3],
+    psi in [-pi/8, pi/8], v in [-1, 5]; grouped by environment (sorted).  One environment: the same
+    state distribution around its goal."""
+    rng = np.random.default_rng(seed * 1000 + rank)
+    env = np.sort(rng.integers(0, len(goals), B))
     gx = np.array([g[0] for g in goals])[env]
     X = np.stack([gx - 25 * rng.random(B), rng.uniform(-3, 3, B), rng.uniform(-np.pi / 8, np.pi / 8, B),
                   rng.uniform(-1, 5, B)], axis=1)
-    offsets = np.searchsorted(env, np.arange(len(ENVS) + 1))
+    offsets = np.searchsorted(env, np.arange(len(goals) + 1))
     return X, env, offsets
 
 
-def build_problems(device):
+def sample_outputfb(rank: int, B: int, goal):
+    """Config-4 inputs: x_true as the config-5 states, x_hat_prev = x_true + N(0, 0.05^2) per
+    component, u_prev = 0, y0 = C x_true (C picks x, y, v: mpc.py:387-389)."""
+    rng = np.random.default_rng(4 * 1000 + rank)
+    gx = goal[0]
+    xt = np.stack([gx - 25 * rng.random(B), rng.uniform(-3, 3, B), rng.uniform(-np.pi / 8, np.pi / 8, B),
+                   rng.uniform(-1, 5, B)], axis=1)
+    xhat = xt + rng.normal(0.0, 0.05, (B, 4))
+    return xt, xhat, np.zeros((B, 2)), xt[:, [0, 1, 3]].copy()
+
+
+def build_controllers(envs, N, device):
     import contextlib
-    from carmpc_amd.environments import ENVIRONMENTS
     from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE
-    from carmpc_amd.mpc import MPCStateFB
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.mpc import MPCOutputFB, MPCStateFB
     ctrls = []
     with contextlib.redirect_stdout(sys.stderr):          # keep stdout to the one JSON line
-        for name in ENVS:
-            c = MPCStateFB(DT_CONTROL, N_HOR, LINEARIZE_STATE, LINEARIZE_INPUT, env=ENVIRONMENTS[name](),
-                           terminal_set_dir=os.path.join(REPO, "terminal_sets"), device=device)
-            c.qp  # assemble on the device now
+        for name in envs:
+            kw = dict(env=ENVIRONMENTS[name](), terminal_set_dir=os.path.join(REPO, "terminal_sets"), device=device)
+            c = MPCStateFB(DT_CONTROL, N, LINEARIZE_STATE, LINEARIZE_INPUT, **kw)
+            c.qp  # assemble now
             ctrls.append(c)
     return ctrls
 
 
-def cpu_baseline(ctrls, X, env, offsets, sample: int, threads: int):
-    """The oracle's C restatement of the same IPM (oracle/ipm.c, OpenMP), on a bounded sample."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def oracle_sample(envs, N, X, offsets, sample: int, threads: int, xref=None):
+    """The oracle's C restatement of the dense IPM (oracle/ipm.c) on a bounded, equal-per-environment
+    sample of this shard: the CPU baseline and I_ref (the oracle's iteration counts, so the
+    canonical flop count does not depend on the kernel being measured)."""
     from oracle import assembly as oa
     from oracle.cpu import CpuProblem
-    idx = np.concatenate([np.arange(offsets[j], min(offsets[j + 1], offsets[j] + sample // len(ENVS)))
-                          for j in range(len(ENVS))])
-    total_t, total_n, iters = 0.0, 0, {}
-    for j, name in enumerate(ENVS):
-        sel = idx[(idx >= offsets[j]) & (idx < offsets[j + 1])]
-        cp = CpuProblem(oa.build(name, N_HOR, terminal_set_dir=os.path.join(REPO, "terminal_sets")))
-        cp.solve(X[sel[:64]], threads=threads)                       # warm
+    per = max(1, sample // len(envs))
+    res = {"threads": threads, "n": 0, "t_all": 0.0, "n1": 0, "t_one": 0.0, "iters": {}}
+    for j, name in enumerate(envs):
+        sel = np.arange(offsets[j], min(offsets[j + 1], offsets[j] + per))
+        if len(sel) == 0:
+            res["iters"][name] = 0.0
+            continue
+        cp = CpuProblem(oa.build(name, N, terminal_set_dir=os.path.join(REPO, "terminal_sets")))
+        xr = None if xref is None else np.ascontiguousarray(np.broadcast_to(xref, (len(sel), 4)))
+        cp.solve(X[sel[:64]], xr[:64] if xr is not None else None, threads=threads)      # warm
         t0 = time.perf_counter()
-        _, st, it = cp.solve(X[sel], threads=threads)
-        total_t += time.perf_counter() - t0
-        total_n += len(sel)
-        iters[name] = (float(it[st == 0].mean()) if (st == 0).any() else 0.0, float(it.mean()))
-    return total_n / total_t, total_n, iters
+        _, st, it = cp.solve(X[sel], xr, threads=threads)
+        res["t_all"] += time.perf_counter() - t0
+        res["n"] += len(sel)
+        res["iters"][name] = float(it.mean())
+        one = sel[:max(64, len(sel) // 16)]
+        t0 = time.perf_counter()
+        cp.solve(X[one], xr[:len(one)] if xr is not None else None, threads=1)
+        res["t_one"] += time.perf_counter() - t0
+        res["n1"] += len(one)
+    return res
 
 
-def main():
+def product_cpu_sample(ctrls, X, offsets, sample: int, threads: int, xref=None):
+    """The library's own CPU QP path (carmpc_cpu_solve_batch, the stage-form IPM) on the same sample."""
+    from carmpc_amd.qp import CpuQPProblem
+    per = max(1, sample // len(ctrls))
+    n, t_all = 0, 0.0
+    for j, c in enumerate(ctrls):
+        sel = np.arange(offsets[j], min(offsets[j + 1], offsets[j] + per))
+        if len(sel) == 0:
+            continue
+        rows, rhs = c._stage_rows()
+        qp = CpuQPProblem(N=c.N, A=c.A, B=c.B, Q=c.Q, R=c.R, P=c.P, goal=c.goal, state_A=rows, state_b=rhs,
+                          term_A=c.term_set_A[:, -4:], term_b=c.term_set_b, u_lower=c.input_lower,
+                          u_upper=c.input_upper)
+        qp.solve(X[sel[:64]], xref, threads=threads)
+        t0 = time.perf_counter()
+        qp.solve(X[sel], xref, threads=threads)
+        t_all += time.perf_counter() - t0
+        n += len(sel)
+    return n / t_all if t_all > 0 else 0.0
+
+
+class GpuBackend:
+    """The device path: torch tensors as buffers, the C ABI for every kernel launch."""
+    name = "gpu"
+
+    def __init__(self, args, local_rank):
+        import torch
+        self.torch = torch
+        self.device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(self.device)
+        self.stream = torch.cuda.current_stream()
+        self.args = args
+
+    def setup(self, ctrls, kind, X, offsets, extra):
+        torch = self.torch
+        from carmpc_amd.qp import SolverSettings
+        self.settings = SolverSettings(kernel=self.args.kernel)
+        self.probs = [c.qp for c in ctrls]
+        self.offsets = offsets
+        self.kind = kind
+        B = X.shape[0]
+        self.Xd = torch.as_tensor(X).to(self.device)
+        self.u = torch.zeros((B, self.probs[0].n), dtype=torch.float64, device=self.device)
+        self.st = torch.empty(B, dtype=torch.int32, device=self.device)
+        self.it = torch.empty(B, dtype=torch.int32, device=self.device)
+        if kind == "outputfb":
+            xhat0, uprev, y, xref = extra
+            self.xhat0 = torch.as_tensor(xhat0).to(self.device)
+            self.xhat = torch.empty_like(self.xhat0)
+            self.uprev = torch.as_tensor(uprev).to(self.device)
+            self.y = torch.as_tensor(y).to(self.device)
+            self.xref = torch.as_tensor(np.ascontiguousarray(np.broadcast_to(xref, (B, 4)))).to(self.device)
+            from carmpc_amd.mpc import MPCOutputFB
+            self.C, self.L = MPCOutputFB.C_OUT, MPCOutputFB.L_GAIN
+        torch.cuda.synchronize()
+        return [self.settings.kernel or p.kernel for p in self.probs]
+
+    def step(self):
+        from carmpc_amd.qp import solve_segments
+        if self.kind == "outputfb":
+            # MPCOutputFB.step (mpc.py:450-478): observer on the previous estimate, then the QP at it
+            self.xhat.copy_(self.xhat0)
+            self.probs[0].observe(self.y, self.xhat, self.uprev, self.C, self.L, stream=self.stream)
+            self.probs[0].solve(self.xhat, self.xref, settings=self.settings, out=(self.u, self.st, self.it),
+                                stream=self.stream)
+        elif self.args.per_problem_launches or len(self.probs) == 1:
+            for j, p in enumerate(self.probs):
+                sl = slice(int(self.offsets[j]), int(self.offsets[j + 1]))
+                p.solve(self.Xd[sl], settings=self.settings, out=(self.u[sl], self.st[sl], self.it[sl]), stream=self.stream)
+        else:
+            solve_segments(self.probs, self.offsets, self.Xd, settings=self.settings, stream=self.stream,
+                           out=(self.u, self.st, self.it))
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def timed_steps(self, steps):
+        """K steps with HIP events on the launch stream around each step's device work."""
+        torch = self.torch
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        for a, b in evs:
+            a.record(self.stream)
+            self.step()
+            b.record(self.stream)
+        return evs
+
+    def device_ms(self, evs):
+        return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    def results(self):
+        return self.st.cpu().numpy(), self.it.cpu().numpy()
+
+    def e2e_qps(self, X):
+        """PCIe-inclusive rate: H2D of x0, the solve, D2H of u and status between pinned host buffers."""
+        torch = self.torch
+        if self.kind == "outputfb":
+            return None
+        Xh = torch.as_tensor(X).pin_memory()
+        uh = torch.empty(self.u.shape, dtype=self.u.dtype).pin_memory()
+        sh = torch.empty(self.st.shape, dtype=self.st.dtype).pin_memory()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            self.Xd.copy_(Xh, non_blocking=True)
+            self.step()
+            uh.copy_(self.u, non_blocking=True)
+            sh.copy_(self.st, non_blocking=True)
+        torch.cuda.synchronize()
+        return 3 * X.shape[0] / (time.perf_counter() - t0)
+
+
+class CpuBackend:
+    """The library's CPU QP path (carmpc_cpu_solve_batch) under the same control flow."""
+    name = "cpu"
+
+    def __init__(self, args, local_rank):
+        self.args = args
+        self.device = "cpu"
+
+    def setup(self, ctrls, kind, X, offsets, extra):
+        from carmpc_amd.qp import SolverSettings
+        self.settings = SolverSettings()
+        self.probs = [c.qp for c in ctrls]
+        self.ctrls, self.kind, self.X, self.offsets, self.extra = ctrls, kind, X, offsets, extra
+        B = X.shape[0]
+        self.u = np.zeros((B, self.probs[0].n))
+        self.st = np.zeros(B, np.int32)
+        self.it = np.zeros(B, np.int32)
+        return [0 for _ in self.probs]
+
+    def step(self):
+        thr = self.args.cpu_threads
+        if self.kind == "outputfb":
+            xhat0, uprev, y, xref = self.extra
+            c = self.ctrls[0]
+            from carmpc_amd.mpc import MPCOutputFB
+            C, L = MPCOutputFB.C_OUT, MPCOutputFB.L_GAIN
+            xhat = xhat0 @ c.A.T + uprev @ c.B.T + (y - xhat0 @ C.T) @ L.T          # mpc.py:448, batched
+            self.u, self.st, self.it = self.probs[0].solve(xhat, xref.reshape(1, 4), self.settings, threads=thr)
+            return
+        for j, p in enumerate(self.probs):
+            sl = slice(int(self.offsets[j]), int(self.offsets[j + 1]))
+            self.u[sl], self.st[sl], self.it[sl] = p.solve(self.X[sl], settings=self.settings, threads=thr)
+
+    def sync(self):
+        pass
+
+    def timed_steps(self, steps):
+        out = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            self.step()
+            out.append(time.perf_counter() - t0)
+        return out
+
+    def device_ms(self, evs):
+        return float(np.mean(evs)) * 1e3
+
+    def results(self):
+        return self.st, self.it
+
+    def e2e_qps(self, X):
+        return None
+
+
+def run(args, backend_cls=None) -> dict | None:
+    """The benchmark's control flow; returns the result line on rank 0 (None elsewhere).
+    ``backend_cls`` is injectable so the distributed flow can run anywhere."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # one process per GPU; ranks never exchange problem data.  The barrier and the max of the
+        # wall times go over gloo on host tensors.
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    if backend_cls is None:
+        backend_cls = CpuBackend if args.backend == "cpu" else GpuBackend
+    be = backend_cls(args, local)
+
+    envs, N, default_B, kind, wname = WORKLOADS[args.workload]
+    B = args.per_gpu or default_B
+    ctrls = build_controllers(envs, N, be.device)
+    goals = [c.goal for c in ctrls]
+    extra = xref = None
+    if kind == "outputfb":
+        xt, xhat0, uprev, y = sample_outputfb(rank, B, goals[0])
+        from carmpc_amd.mpc import MPCOutputFB
+        xref = goals[0]           # optimal target selection: the unique steady state is the goal (mpc.py:413-437)
+        extra = (xhat0, uprev, y, xref)
+        # the QP is solved at the observer's estimate: the oracle sample uses the same states
+        X = xhat0 @ ctrls[0].A.T + uprev @ ctrls[0].B.T + (y - xhat0 @ MPCOutputFB.C_OUT.T) @ MPCOutputFB.L_GAIN.T
+        offsets = np.array([0, B])
+    else:
+        X, _env, offsets = sample_shard(rank, B, goals, seed={"config5": 5, "config3": 3, "config2": 2}[args.workload])
+    kernels = be.setup(ctrls, kind, X, offsets, extra)
+
+    for _ in range(args.warmup):
+        be.step()
+    be.sync()
+    if dist is not None:
+        dist.barrier()
+    be.sync()
+    t0 = time.perf_counter()
+    evs = be.timed_steps(args.steps)
+    be.sync()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    wall_max = wall
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)          # host tensor: gloo
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall_max = float(t.item())
+    kern_ms = be.device_ms(evs)
+    e2e = be.e2e_qps(X)
+    st_np, it_np = be.results()
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return None
+
+    value = B * world * args.steps / wall_max
+    probs = be.probs
+    used = sorted(set(kernels))
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "QP/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded state distribution of the configuration)",
+        "config": {"workload": wname, "per_gpu_batch": B, "global_batch": B * world, "envs": list(envs), "N": N,
+                   "n": 2 * N, "p_qp_rows": [p.p for p in probs],
+                   "kernel": ("carmpc_cpu_solve_batch (host stage-form IPM)" if be.name == "cpu"
+                              else "; ".join(KDESC.get(k, str(k)) for k in used)),
+                   "step": ("observer kernel + QP solve (MPCOutputFB.step)" if kind == "outputfb" else "QP solve"),
+                   "backend": be.name, "parallelism": f"shard{world} (no data-path collective)"},
+        "status_split": {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
+                                                                         "numerical"))},
+        "iters_mean_optimal": float(it_np[st_np == 0].mean()) if (st_np == 0).any() else 0.0,
+    }
+    if e2e is not None:
+        out["e2e_qps_pcie_inclusive"] = round(e2e * world, 1)
+
+    # CPU baseline and I_ref: the oracle on a bounded sample of rank 0's shard
+    seg = np.diff(offsets)
+    if not args.no_cpu:
+        thr = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        osr = oracle_sample(envs, N, X, offsets, args.cpu_sample, thr, xref)
+        I_ref = osr["iters"]
+        prod = product_cpu_sample(ctrls, X, offsets, args.cpu_sample, thr, None if xref is None else np.asarray(xref).reshape(1, 4))
+        out["cpu_baseline"] = {
+            "value": round(osr["n"] / osr["t_all"], 1), "unit": "QP/s", "cores": thr, "kind": "port",
+            "sample": f"{osr['n']} instances of rank 0's shard (equal per environment), oracle/ipm.c (dense Mehrotra "
+                      f"IPM, the algorithm of the canonical flop count), OpenMP x{thr}",
+            "cpu_model": cpu_model(),
+            "single_thread": {"value": round(osr["n1"] / osr["t_one"], 1), "cores": 1, "sample": f"{osr['n1']} instances"},
+            "product_cpu_path": {"value": round(prod, 1), "cores": thr,
+                                 "what": "carmpc_cpu_solve_batch (the library's stage-form IPM on the host), same sample"},
+        }
+        iref_src = "oracle/ipm.c on the cpu_baseline sample (rank 0)"
+    else:
+        I_ref = {envs[j]: float(it_np[offsets[j]:offsets[j + 1]].mean()) if seg[j] else 0.0 for j in range(len(envs))}
+        iref_src = "--no-cpu: this run's own iteration counts (not a valid roofline numerator)"
+    if be.name == "gpu":
+        canon = [seg[j] * I_ref[envs[j]] * probs[j].canonical_flops_per_iter() for j in range(len(envs))]
+        execd = [float(it_np[offsets[j]:offsets[j + 1]].sum()) * probs[j].executed_flops_per_iter(kernels[j])
+                 for j in range(len(envs))]
+        flops_step = float(sum(canon))
+        achieved = flops_step / (kern_ms * 1e-3) / 1e12
+        exec_tf = sum(execd) / (kern_ms * 1e-3) / 1e12
+        per_qp = 32 + 4 + 8 * 2 * N + 4 + 4 + (24 + 32 + 16 + 32 if kind == "outputfb" else 0)
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                with open(args.traffic_json) as f:
+                    ent = json.load(f).get(args.workload + ":" + "+".join(KNAME.get(k, str(k)) for k in used))
+                if ent is not None and ent.get("per_gpu_batch") == B:
+                    traffic = ent.get("hbm_bytes_per_step")
+            except Exception:
+                traffic = None
+        out["roofline"] = {
+            "bound": "fp64_valu",
+            "compute": "FP64: vector FMA (row phases) and v_mfma_f64_4x4x4 (stage recursions); both rates equal the "
+                       "78.6 TFLOP/s peak",
+            "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+            "frac_is": "canonical dense-IPM flops (p n^2 + n^3/3 + 6 n^2 + 12 p n per iteration) x the oracle's "
+                       "iteration counts / kernel time / peak: a normalised rate, NOT hardware utilisation",
+            "executed_frac": round(exec_tf / FP64_PEAK_TFLOPS, 5),
+            "executed_TFLOPs": round(exec_tf, 4),
+            "executed_is": "flops the stage-form kernel actually performs (useful lanes only) x its own iteration "
+                           "counts / kernel time / peak: the hardware FP64 utilisation",
+            "traffic": traffic, "algorithmic_bytes_per_step": B * per_qp,
+            "algorithmic_hbm_GBps": round(B * per_qp / (kern_ms * 1e-3) / 1e9, 3),
+            "hbm_frac": round(B * per_qp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
+            "kernel_ms_per_step": round(kern_ms, 4), "canonical_flops_per_step": flops_step,
+            "executed_flops_per_step": float(sum(execd)),
+            "timing": "HIP events on the launch stream around each step's device work, mean over the timed steps",
+            "I_ref": I_ref, "I_ref_source": iref_src,
+            "launches": [{"env": envs[j], "kernel": KNAME.get(kernels[j], str(kernels[j])), "instances": int(seg[j]),
+                          "canonical_flops": canon[j]} for j in range(len(envs))],
+        }
+    else:
+        out["roofline"] = None
+        out["cpu_step_ms"] = round(kern_ms, 3)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--per-gpu", type=int, default=PER_GPU)
+    ap.add_argument("--workload", default="config5", choices=sorted(WORKLOADS))
+    ap.add_argument("--per-gpu", type=int, default=0, help="instances per rank (default: the configuration's batch)")
+    ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--cpu-threads", type=int, default=0, help="--backend cpu: threads per rank (0 = all)")
     ap.add_argument("--cpu-sample", type=int, default=24576)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--serial-segments", action="store_true",
-                    help="launch the environment segments one after another instead of concurrently")
-    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 3 dense 1-wave/SIMD, 7 riccati)")
+    ap.add_argument("--per-problem-launches", action="store_true",
+                    help="one carmpc_solve_batch launch per environment instead of one carmpc_solve_segments call")
+    ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 7 riccati)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-
-    from carmpc_amd.qp import SolverSettings
-    settings = SolverSettings(kernel=args.kernel)
-    ctrls = build_problems(device)
-    probs = [c.qp for c in ctrls]
-    goals = [c.goal for c in ctrls]
-    X, env, offsets = sample_shard(rank, args.per_gpu, goals)
-    Xd = torch.as_tensor(X).to(device)
-    B = args.per_gpu
-    u = torch.zeros((B, 40), dtype=torch.float64, device=device)
-    st = torch.empty(B, dtype=torch.int32, device=device)
-    it = torch.empty(B, dtype=torch.int32, device=device)
-    segs = [(probs[j], slice(int(offsets[j]), int(offsets[j + 1]))) for j in range(len(ENVS))]
-    kernels = [settings.kernel or p.kernel for p in probs]
-    torch.cuda.synchronize()
-
-    stream = torch.cuda.current_stream()
-
-    from carmpc_amd import _native
-    from carmpc_amd.qp import solve_segments
-    _native.load().carmpc_set_serial_segments(1 if args.serial_segments else 0)
-
-    def step(events=None):
-        # one pass of the hot path: the three environment segments in one carmpc_solve_segments
-        # call (launches forked onto side streams and joined back; --serial-segments: one by one)
-        if args.serial_segments:
-            for j, (p, sl) in enumerate(segs):
-                if events is not None:
-                    events[j].record(stream)
-                p.solve(Xd[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
-            if events is not None:
-                events[len(segs)].record(stream)
-            return
-        if events is not None:
-            events[0].record(stream)
-        solve_segments(probs, offsets, Xd, settings=settings, stream=stream, out=(u, st, it))
-        if events is not None:
-            events[len(segs)].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(segs) + 1)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    if args.serial_segments:
-        seg_ms = np.array([[e[j].elapsed_time(e[j + 1]) for j in range(len(segs))] for e in evs]).mean(axis=0)
-        kern_ms = float(seg_ms.sum())
-    else:
-        # device span of the solve call (fork -> join on the launch stream): the three launches overlap
-        kern_ms = float(np.mean([e[0].elapsed_time(e[len(segs)]) for e in evs]))
-        seg_ms = None
-    t = torch.tensor([wall], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
-
-    # end-to-end (PCIe-inclusive) figure: H2D x0, solve, D2H u and status between pinned host
-    # buffers, mean of 3 passes -- reported, never `value`
-    Xh = torch.as_tensor(X).pin_memory()
-    uh = torch.empty(u.shape, dtype=u.dtype).pin_memory()
-    sh = torch.empty(st.shape, dtype=st.dtype).pin_memory()
-    Xe = torch.empty_like(Xh, device=device)
-    torch.cuda.synchronize()
-    te = time.perf_counter()
-    for _ in range(3):
-        with torch.cuda.stream(stream):
-            Xe.copy_(Xh, non_blocking=True)
-        if args.serial_segments:
-            for p, sl in segs:
-                p.solve(Xe[sl], settings=settings, out=(u[sl], st[sl], it[sl]), stream=stream)
-        else:
-            solve_segments(probs, offsets, Xe, settings=settings, stream=stream, out=(u, st, it))
-        with torch.cuda.stream(stream):
-            uh.copy_(u, non_blocking=True)
-            sh.copy_(st, non_blocking=True)
-    torch.cuda.synchronize()
-    e2e = 3 * B / (time.perf_counter() - te)
-
-    st_np = st.cpu().numpy(); it_np = it.cpu().numpy()
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-    total = B * world * args.steps
-    value = total / wall_max
-    status_split = {s: int((st_np == k).sum()) for k, s in enumerate(("optimal", "primal_infeasible", "max_iter",
-                                                                      "numerical"))}
-    kname = {1: "ipm_dense", 2: "ipm_staged", 3: "ipm_dense_4wave", 4: "ipm_staged_readlane", 5: "ipm_staged_4wave", 6: "ipm_staged_ldl",
-             7: "ipm_riccati"}
-    kdesc = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
-             2: "ipm_staged (wavefront per QP, stage-structured G/H products and Riccati-style M build)",
-             3: "ipm_dense, 4 waves per workgroup",
-             4: "ipm_staged with the readlane-broadcast Cholesky (A/B variant)",
-             5: "ipm_staged, 4 waves per workgroup (512 registers per wave)",
-             6: "ipm_staged with the square-root-free LDL' (A/B variant)",
-             7: "ipm_riccati (16 lanes per QP, 4 QPs per wavefront, row state in registers, stage-form Riccati "
-                "factorization and solves, per-group instance refill)"}
-    used = sorted(set(kernels))
-    out = {
-        "metric": "QP solves/sec (batched MPC steps), N=20 n=4 m=2, at 1/2/4/8 MI355X",
-        "value": round(value, 1), "unit": "QP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall_max / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded config-5 state distribution)",
-        "config": {"workload": "config5_mixed_road_envs_N20_weak", "per_gpu_batch": B,
-                   "global_batch": B * world, "envs": list(ENVS), "N": N_HOR, "n": 40,
-                   "p_qp_rows": [p.p for p in probs], "kernel": "; ".join(kdesc[k] for k in used),
-                   "parallelism": f"shard{world} (no data-path collective)"},
-        "status_split": status_split,
-        "gpu_iters_mean": float(it_np[st_np == 0].mean()),
-        "e2e_qps_pcie_inclusive": round(e2e * world, 1),
-    }
-    # roofline: canonical FP64 flops (SURVEY §8d) with I_ref from the oracle on a sample of this batch
-    seg = np.diff(offsets)
-    if not args.no_cpu and world == 1:
-        thr = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-        cpu_qps, ncpu, iref = cpu_baseline(ctrls, X, env, offsets, args.cpu_sample, thr)
-        out["cpu_baseline"] = {"value": round(cpu_qps, 1), "unit": "QP/s", "cores": thr, "kind": "port",
-                               "sample": f"{ncpu} instances of this shard (equal per env), oracle/ipm.c "
-                                         f"OpenMP x{thr}, {platform.processor() or platform.machine()}"}
-        I_ref = {k: v[1] for k, v in iref.items()}
-        iref_src = "oracle/ipm.c on the cpu_baseline sample"
-    else:
-        I_ref = {ENVS[j]: float(it_np[offsets[j]:offsets[j + 1]].mean()) for j in range(len(ENVS))}
-        iref_src = "GPU iteration counts of this batch"
-    canon = [seg[j] * I_ref[ENVS[j]] * probs[j].canonical_flops_per_iter() for j in range(len(ENVS))]
-    execd = [float(it_np[offsets[j]:offsets[j + 1]].sum()) * probs[j].executed_flops_per_iter(kernels[j])
-             for j in range(len(ENVS))]
-    flops_step = float(sum(canon))
-    achieved = flops_step / (kern_ms * 1e-3) / 1e12
-    bytes_step = B * (32 + 4 + 8 * 40 + 4 + 4)     # x0 + env in; u + status + iters out
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            key = "+".join(kname[k] for k in used)
-            ent = tj.get(key)
-            if ent is not None and ent.get("per_gpu_batch") == B:
-                traffic = ent.get("hbm_bytes_per_step")
-        except Exception:
-            traffic = None
-    if seg_ms is not None:
-        launches = [{"env": ENVS[j], "kernel": kname[kernels[j]], "instances": int(seg[j]), "ms": round(float(seg_ms[j]), 4),
-                     "canonical_TFLOPs": round(canon[j] / (seg_ms[j] * 1e-3) / 1e12, 4),
-                     "executed_TFLOPs": round(execd[j] / (seg_ms[j] * 1e-3) / 1e12, 4)} for j in range(len(ENVS))]
-    else:
-        launches = [{"env": ENVS[j], "kernel": kname[kernels[j]], "instances": int(seg[j]),
-                     "canonical_flops": canon[j]} for j in range(len(ENVS))]
-    out["roofline"] = {"bound": "mfma", "compute": "fp64 FMA (vector; FP64 vector peak == FP64 matrix peak)",
-                       "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                       "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": traffic,
-                       "flops": "canonical dense-IPM count (SURVEY §8d) x I_ref",
-                       "kernel_ms_per_step": round(kern_ms, 4), "canonical_flops_per_step": flops_step,
-                       "timing": ("per-launch HIP events, launches back to back on one stream" if seg_ms is not None
-                                  else "HIP events around the carmpc_solve_segments call on the launch stream: the "
-                                       "span of the 3 concurrent launches (fork/join over side streams)"),
-                       "executed_flops_per_step": float(sum(execd)),
-                       "executed_TFLOPs": round(sum(execd) / (kern_ms * 1e-3) / 1e12, 4),
-                       "I_ref": I_ref, "I_ref_source": iref_src, "launches": launches,
-                       "algorithmic_hbm_GBps": round(bytes_step / (kern_ms * 1e-3) / 1e9, 3)}
-    print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def main(argv=None):
+    out = run(parse_args(argv))
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

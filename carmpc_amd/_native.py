@@ -1,8 +1,9 @@
 """ctypes binding of ``libcarmpc.so`` -- the C ABI declared in ``include/carmpc.h``.
 
 The library is built in-tree (``python -m carmpc_amd.build`` or
-``__graft_entry__.build()``).  There is no fallback: if the library or a GPU
-is missing, every solve entry point raises ``CarMPCNativeError``.
+``__graft_entry__.build()``).  If the library is missing every entry point raises
+``CarMPCNativeError``; the device entry points need a GPU, the ``carmpc_cpu_*`` twins
+(the host's CPU QP path, as in the reference) do not.
 """
 from __future__ import annotations
 
@@ -28,7 +29,9 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
            "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
            "carmpc_hetero_get", "carmpc_set_serial_segments", "carmpc_solve_batch_noalloc",
-           "carmpc_problem_set_observer")
+           "carmpc_problem_set_observer", "carmpc_cpu_problem_create", "carmpc_cpu_problem_destroy",
+           "carmpc_cpu_problem_info", "carmpc_cpu_problem_set_disturbance", "carmpc_cpu_solve_batch",
+           "carmpc_cpu_solve_batch_dist")
 
 # outcomes of carmpc_closed_loop_batch (carmpc.h)
 LOOP_RUNNING, LOOP_REACHED, LOOP_INFEASIBLE, LOOP_INPUT_VIOLATION, LOOP_TIMEOUT, LOOP_SOLVER_FAILURE = -1, 0, 1, 2, 3, 4
@@ -98,6 +101,13 @@ def load():
         "carmpc_solve_batch": ([vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_solve_batch_noalloc": ([vp, i64, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_problem_set_observer": ([vp, i32, dp, dp, dp, dp, dp], ctypes.c_int),
+        "carmpc_cpu_problem_create": ([ctypes.POINTER(ModelDesc), ctypes.POINTER(vp)], ctypes.c_int),
+        "carmpc_cpu_problem_destroy": ([vp], None),
+        "carmpc_cpu_problem_info": ([vp, ip, ip, ip, ip, ip], ctypes.c_int),
+        "carmpc_cpu_problem_set_disturbance": ([vp, dp], ctypes.c_int),
+        "carmpc_cpu_solve_batch": ([vp, i64, dp, dp, dp, ip, ip, ctypes.POINTER(Settings), i32], ctypes.c_int),
+        "carmpc_cpu_solve_batch_dist": ([vp, i64, dp, dp, dp, dp, ip, ip, ctypes.POINTER(Settings), i32],
+                                        ctypes.c_int),
         "carmpc_solve_segments": ([ctypes.POINTER(vp), i32, ctypes.POINTER(i64), vp, vp, vp, i64, vp, vp,
                                    ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_observer_batch": ([vp, i64, vp, i32, dp, dp, vp, vp, i64, vp], ctypes.c_int),

@@ -12,7 +12,7 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libcarmpc.so")
-SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip", "noalloc.hip"]
+SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip", "noalloc.hip", "cpu_ipm.hip"]
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
 # -packed-fp32-ops off: hipcc -O3 forms v_pk_*_f32 from ordinary float code by itself and some of
 # their forms have given wrong results on these GPUs; the flag only concerns the device pass (the
@@ -33,11 +33,15 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def _stale(obj, src):
-    if not os.path.exists(obj):
+def _stale(obj, src, cmd):
+    """Rebuild when the object is missing, older than its sources, or was built by another command line."""
+    if not os.path.exists(obj) or not os.path.exists(obj + ".cmd"):
         return True
+    with open(obj + ".cmd") as f:
+        if f.read() != " ".join(cmd):
+            return True
     deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h"),
-            os.path.join(REPO, "include", "carmpc.h"), os.path.abspath(__file__)]
+            os.path.join(REPO, "include", "carmpc.h")]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
@@ -53,11 +57,13 @@ def build(verbose: bool = True, jobs: int = 4, variant: str = "") -> str:
     def compile_one(src):
         s = os.path.join(CSRC, src)
         o = os.path.join(obj_dir, src.replace(".hip", ".o"))
-        if _stale(o, s):
-            cmd = [hipcc, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o]
+        cmd = [hipcc, *FLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", s, "-o", o]
+        if _stale(o, s, cmd):
             if verbose:
                 print(" ".join(cmd), flush=True)
             subprocess.run(cmd, check=True)
+            with open(o + ".cmd", "w") as f:
+                f.write(" ".join(cmd))
         return o
 
     with ThreadPoolExecutor(max_workers=jobs) as ex:

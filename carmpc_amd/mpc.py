@@ -14,8 +14,11 @@ the work happens:
   optimal-target QP (mpc.py:413-437), which is constant, is solved once in
   closed form instead of every step.
 
-There is no CPU solve path: without the HIP library or a GPU, ``step`` raises
-``CarMPCNativeError``.
+Without a GPU (``torch.cuda.is_available()`` false, or ``device="cpu"``) the controllers solve
+the same QP on the host's cores through the library's ``carmpc_cpu_*`` entry points -- the
+reference's controllers are CPU programs (mpc.py:334-335), and its plumbing configuration
+(run_MPCStateFB, N = 10) runs without a GPU.  With a GPU present the device path is always used;
+a missing library raises ``CarMPCNativeError`` either way.
 """
 from __future__ import annotations
 
@@ -183,9 +186,13 @@ class MPC:
     # ------------------------------------------------------------ device QP
     @property
     def qp(self):
-        """The controller's device QP (assembled by the HIP kernel on first access)."""
+        """The controller's QP: on the device (assembled by the HIP kernel on first access), or the
+        host twin when no GPU is present / ``device="cpu"``."""
         if self._qp is None:
-            from .qp import QPProblem
+            import torch
+            from .qp import CpuQPProblem, QPProblem
+            on_gpu = torch.cuda.is_available() if self.device is None else torch.device(self.device).type == "cuda"
+            QPProblem = QPProblem if on_gpu else CpuQPProblem
             rows, rhs = self._stage_rows() if self.state_constraint_bool else (None, None)
             term_A = term_b = None
             if self.terminal_constraint_bool:
@@ -207,7 +214,16 @@ class MPC:
     H = property(lambda self: self._mats()["H"], doc="condensed Hessian (device-assembled)")
     h = property(lambda self: self._mats()["h"], doc="condensed linear-term matrix (device-assembled)")
 
+    @property
+    def on_cpu(self) -> bool:
+        """True when this controller solves on the host (no GPU present, or device="cpu")."""
+        return self.qp.device.type == "cpu"
+
     def _solve_one(self, x0: np.ndarray, xref: np.ndarray) -> np.ndarray:
+        if self.on_cpu:
+            u, st, _ = self.qp.solve(np.asarray(x0, float).reshape(1, 4), np.asarray(xref, float).reshape(1, 4),
+                                     self.settings)
+            return self._check_status(int(st[0]), u[0])
         import torch
         dev = self.qp.device
         X = torch.as_tensor(np.asarray(x0, dtype=np.float64).reshape(1, 4)).to(dev)
@@ -229,6 +245,11 @@ class MPC:
 
         Returns (u0 (B x nu), u (B x N nu), status (B,)) as device tensors; status
         1 marks states outside the region of attraction.  xref defaults to the goal."""
+        if self.on_cpu:     # host twin: numpy in, numpy out
+            X = np.asarray(x0, dtype=np.float64).reshape(-1, 4)
+            Rf = self.goal.reshape(1, 4) if xref is None else np.asarray(xref, dtype=np.float64).reshape(-1, 4)
+            u, st, _ = self.qp.solve(X, Rf, self.settings)
+            return u[:, :self.nu], u, st
         import torch
         X = torch.as_tensor(x0, dtype=torch.float64).to(self.qp.device).reshape(-1, 4)
         Rf = None
@@ -337,8 +358,14 @@ class MPCOutputFB(MPC):
 
     def step(self, y0) -> np.ndarray:
         """Observer -> target -> QP (mpc.py:450-492), observer and QP on the GPU."""
-        import torch
         qp = self.qp
+        if self.on_cpu:
+            x0 = self.luenberger_observer(np.asarray(y0, dtype=float))          # mpc.py:456-458
+            self._x_est = x0.copy()
+            x_ref, _u_ref = self.optimal_target_selection()
+            u = self._solve_one(x0, x_ref)
+            return self._finish_step(x0, x_ref, u)
+        import torch
         dev = qp.device
         if self._x_dev is None:
             self._x_dev = torch.as_tensor(self._x_est.reshape(1, 4)).to(dev).contiguous()
@@ -352,13 +379,16 @@ class MPCOutputFB(MPC):
         x0 = self._x_dev[0].cpu().numpy()
         self._x_est = x0.copy()
         u = self._check_status(int(st.cpu()[0]), u_all[0].cpu().numpy())
+        self._u_dev = u_all[:, :self.nu].contiguous()
+        return self._finish_step(x0, x_ref, u)
+
+    def _finish_step(self, x0, x_ref, u) -> np.ndarray:
         m = self._mats()
         dx = x0 - x_ref
         self.x_horizon = (m["T"] @ dx + m["S"] @ u).reshape(-1, self.nx) + self.goal      # mpc.py:484-485
         self.u_horizon = u.reshape(-1, 2)
         self.cost = 0.5 * u @ m["H"] @ u + (m["h"] @ dx) @ u                             # mpc.py:478,487
         self.previous_u = u[:self.nu]
-        self._u_dev = u_all[:, :self.nu].contiguous()
         return u[:self.nu]
 
 
@@ -439,8 +469,14 @@ class MPCOutputFBWithDisturbance(MPC):
 
     def step(self, y0) -> np.ndarray:
         """Observer -> QP with the disturbance offset (mpc.py:614-667), both on the GPU."""
-        import torch
         qp = self._qp_dist()
+        if self.on_cpu:
+            x0, d0 = self.luenberger_observer(np.asarray(y0, dtype=float))      # mpc.py:620
+            self.x_estimate, self.d_estimate = x0.copy(), d0
+            u_all, st, _ = qp.solve(x0.reshape(1, 4), self.X_REF.reshape(1, 4), self.settings, dist=np.array([d0]))
+            u = self._check_status(int(st[0]), u_all[0])
+            return self._finish_step(x0, u)
+        import torch
         dev = qp.device
         xh = torch.as_tensor(self.x_estimate.reshape(1, 4)).to(dev).contiguous()
         dh = torch.tensor([float(self.d_estimate)], dtype=torch.float64, device=dev)
@@ -451,6 +487,9 @@ class MPCOutputFBWithDisturbance(MPC):
         self.x_estimate = x0.copy()
         self.d_estimate = float(dh.cpu()[0])
         u = self._check_status(int(st.cpu()[0]), u_all[0].cpu().numpy())
+        return self._finish_step(x0, u)
+
+    def _finish_step(self, x0, u) -> np.ndarray:
         m = self._mats()
         dx = x0 - self.X_REF
         self.x_horizon = (m["T"] @ dx + m["S"] @ u).reshape(-1, self.nx) + self.goal     # mpc.py:659-660

@@ -43,8 +43,8 @@ def _stream_handle(stream: torch.cuda.Stream | None):
 
 def require_gpu(device=None) -> torch.device:
     if not torch.cuda.is_available():
-        raise CarMPCNativeError("carmpc_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
-                                "there is no CPU fallback")
+        raise CarMPCNativeError("this entry point needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                "only the per-step QP has a CPU path (carmpc_amd.qp.CpuQPProblem)")
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     return dev
 
@@ -281,30 +281,159 @@ class QPProblem:
                                                           _stream_handle(stream)), "carmpc_closed_loop_batch")
         return {"state": state, "xhat": xhat, "dhat": dhat, "u": u, "outcome": outcome, "steps": steps}
 
+class CpuQPProblem:
+    """The same condensed QP solved on the host's cores (``carmpc_cpu_*``): the product's CPU QP
+    path, as the reference's controllers have one (cvxpy, lib/mpc.py:334-335).  Used by the
+    controllers when no GPU is present; the arguments are those of ``QPProblem``, batches are
+    numpy arrays (or CPU tensors) and the results numpy arrays."""
+
+    assembled = True
+    kernel = 0
+    device = torch.device("cpu")
+
+    def __init__(self, *, N: int, A, B, Q, R, P, goal, state_A=None, state_b=None, term_A=None, term_b=None,
+                 u_lower=None, u_upper=None, device=None, threads: int = 0):
+        lib = _native.load()
+        A, B, Q, R, P, goal = (_f64(v) for v in (A, B, Q, R, P, goal))
+        nu = B.shape[1]
+        sA = _f64(state_A if state_A is not None else np.zeros((0, NX)))
+        sb = _f64(state_b if state_b is not None else np.zeros(0))
+        tA = _f64(term_A if term_A is not None else np.zeros((0, NX)))
+        tb = _f64(term_b if term_b is not None else np.zeros(0))
+        lo, hi = _f64(u_lower), _f64(u_upper)
+        self._model = (A, B, Q, R, P)
+        d = ModelDesc(N=N, nx=NX, nu=nu, A=_dptr(A), B=_dptr(B), Q=_dptr(Q), R=_dptr(R), P=_dptr(P),
+                      n_state_rows=sA.shape[0], state_A=_dptr(sA), state_b=_dptr(sb),
+                      n_term_rows=tA.shape[0], term_A=_dptr(tA), term_b=_dptr(tb),
+                      u_lower=_dptr(lo), u_upper=_dptr(hi), goal=_dptr(goal))
+        handle = ctypes.c_void_p()
+        check(lib.carmpc_cpu_problem_create(ctypes.byref(d), ctypes.byref(handle)), "carmpc_cpu_problem_create")
+        self._h = handle
+        self.N, self.nu, self.threads = N, nu, threads
+        self.goal = goal.copy()
+        self._rows = (tA, tb, sA, sb)
+        vals = [ctypes.c_int32() for _ in range(5)]
+        check(lib.carmpc_cpu_problem_info(self._h, *[ctypes.byref(v) for v in vals]), "carmpc_cpu_problem_info")
+        self.n, self.p, self.npre, self.nx, _ = (v.value for v in vals)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _native.load().carmpc_cpu_problem_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def matrices(self) -> dict:
+        """T, S, H, h, G, E, w0 built on the host (matrix_gen.py:6-72, mpc.py:196-253), with the
+        keys and row order of ``QPProblem.matrices``."""
+        from .matrix_gen import costgen, predmod
+        A, B, Q, R, P = self._model
+        N = self.N
+        T, S = predmod(A, B, N)
+        H, h, _ = costgen(Q, R, P, T, S, NX)
+        tA, tb, sA, sb = self._rows
+        rows = np.zeros((len(tb) + len(sb) * N, (N + 1) * NX))
+        rows[:len(tb), -NX:] = tA
+        for j, c in enumerate(sA):
+            for i in range(N):
+                rows[len(tb) + j * N + i, (i + 1) * NX:(i + 2) * NX] = c
+        return dict(T=T, S=S, H=H, h=h, G=rows @ S, E=rows @ T, w0=np.concatenate((tb, np.repeat(sb, N))))
+
+    def set_disturbance(self, Bd) -> None:
+        Bd = _f64(Bd).reshape(-1)
+        if Bd.shape != (NX,):
+            raise ValueError("Bd must have nx entries")
+        check(_native.load().carmpc_cpu_problem_set_disturbance(self._h, _dptr(Bd)), "carmpc_cpu_problem_set_disturbance")
+        self.Bd = Bd.copy()
+
+    def solve(self, x0, xref=None, settings: SolverSettings | None = None, dist=None, threads: int | None = None):
+        """(u (B x n), status (B,), iters (B,)) as numpy arrays for the rows of x0 (B x 4)."""
+        def host(a, width):
+            if isinstance(a, torch.Tensor):
+                a = a.detach().cpu().numpy()
+            a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1, width))
+            return a
+        X = host(x0, NX)
+        B = X.shape[0]
+        R = None
+        if xref is not None:
+            R = host(xref, NX)
+            if R.shape[0] == 1 and B > 1:
+                R = np.ascontiguousarray(np.broadcast_to(R, (B, NX)))
+            if R.shape != X.shape:
+                raise ValueError("xref must have the shape of x0")
+        u = np.empty((B, self.n))
+        st = np.empty(B, dtype=np.int32)
+        it = np.empty(B, dtype=np.int32)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        s = (settings or SolverSettings()).c()
+        nthr = self.threads if threads is None else threads
+        lib = _native.load()
+        if dist is None:
+            check(lib.carmpc_cpu_solve_batch(self._h, B, _dptr(X), _dptr(R), _dptr(u), st.ctypes.data_as(ip),
+                                             it.ctypes.data_as(ip), ctypes.byref(s), nthr), "carmpc_cpu_solve_batch")
+        else:
+            dv = host(dist, 1).reshape(-1)
+            if dv.shape[0] != B:
+                raise ValueError("dist must have one entry per instance")
+            check(lib.carmpc_cpu_solve_batch_dist(self._h, B, _dptr(X), _dptr(R), _dptr(dv), _dptr(u),
+                                                  st.ctypes.data_as(ip), it.ctypes.data_as(ip), ctypes.byref(s), nthr),
+                  "carmpc_cpu_solve_batch_dist")
+        return u, st, it
+
+
 def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,
                    settings: SolverSettings | None = None, stream=None, out: tuple | None = None):
-    """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j].  The
-    segments' launches run concurrently on side streams, joined back into ``stream``.
-    ``out`` = (u (B x ld), status, iters) preallocated device tensors."""
+    """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j]; one call
+    solves all segments (stream-ordered on ``stream``).  ``xref`` is B x 4 or 1 x 4;
+    ``out`` = (u (B x ld, unit column stride), status (B,), iters (B,)) preallocated device tensors."""
+    if not problems:
+        raise ValueError("no problems")
     dev = problems[0].device
+    if any(p.device != dev for p in problems):
+        raise ValueError("all problems of one call must live on one device")
     x0 = _as_dev(x0, dev)
     B = x0.shape[0]
+    offs_l = [int(o) for o in offsets]
+    if len(offs_l) != len(problems) + 1:
+        raise ValueError(f"offsets must have len(problems) + 1 = {len(problems) + 1} entries")
+    if offs_l[0] < 0 or offs_l[-1] > B or any(b < a for a, b in zip(offs_l, offs_l[1:])):
+        raise ValueError(f"offsets must be non-decreasing within [0, {B}]")
+    ld_min = max(p.n for p in problems)
+    s_obj = stream if stream is not None else torch.cuda.current_stream(dev)
     if out is None:
-        ld = max(p.n for p in problems)
-        u = torch.zeros((B, ld), dtype=torch.float64, device=dev)
-        st = torch.empty(B, dtype=torch.int32, device=dev)
-        it = torch.empty(B, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(s_obj):      # the fill below must be ordered before the solve on `stream`
+            u = torch.zeros((B, ld_min), dtype=torch.float64, device=dev)
+            st = torch.empty(B, dtype=torch.int32, device=dev)
+            it = torch.empty(B, dtype=torch.int32, device=dev)
     else:
         u, st, it = out
-        ld = u.stride(0)
+        if u.dtype != torch.float64 or u.dim() != 2 or u.shape[0] < offs_l[-1] or u.shape[1] < ld_min or \
+                u.stride(1) != 1 or u.device != dev:
+            raise ValueError(f"out[0] must be float64 on {dev}, at least {offs_l[-1]} x {ld_min}, unit column stride")
+        for t, nm in ((st, "status"), (it, "iters")):
+            if t.dtype != torch.int32 or t.dim() != 1 or t.shape[0] < offs_l[-1] or not t.is_contiguous() or t.device != dev:
+                raise ValueError(f"out {nm} must be a contiguous int32 vector on {dev} with at least {offs_l[-1]} entries")
+    ld = u.stride(0)
+    xr = None
+    if xref is not None:
+        xr = _as_dev(xref, dev)
+        if xr.shape[0] == 1 and B > 1:
+            xr = xr.expand(B, NX).contiguous()
+        if xr.shape != x0.shape:
+            raise ValueError("xref must be B x 4 (or 1 x 4)")
     handles = (ctypes.c_void_p * len(problems))(*[p._h.value for p in problems])
-    offs = (ctypes.c_int64 * (len(problems) + 1))(*[int(o) for o in offsets])
+    offs = (ctypes.c_int64 * (len(problems) + 1))(*offs_l)
     s = (settings or SolverSettings()).c()
-    xr = None if xref is None else _as_dev(xref, dev)
     with torch.cuda.device(dev):
         check(_native.load().carmpc_solve_segments(handles, len(problems), offs, _tptr(x0), _tptr(xr), _tptr(u), ld,
-                                                   _tptr(st), _tptr(it), ctypes.byref(s), _stream_handle(stream)),
+                                                   _tptr(st), _tptr(it), ctypes.byref(s), _stream_handle(s_obj)),
               "carmpc_solve_segments")
+    for t in (x0, xr, u, st, it):
+        if t is not None:
+            t.record_stream(s_obj)
     return u, st, it
 
 

@@ -299,6 +299,30 @@ int carmpc_hetero_get(const carmpc_hetero* h, double* A, double* B, double* P, d
                       int32_t* p, int32_t* npre, double* G, double* H, double* hq, double* w0, double* E,
                       int64_t* dims);
 
+/* ---- CPU twins: the same QP on the host's cores -----------------------------------------
+ * The reference solves its per-step QP on the CPU (cp.Problem(...).solve(), lib/mpc.py:334-335,
+ * 477-478, 652-653).  These entry points are that path for hosts without a GPU and the plumbing
+ * configuration "run_MPCStateFB, N = 10, CPU QP path": the same stage-form interior-point method
+ * as the device kernel (tolerances, row normalisation, x0-only preconditions, infeasibility
+ * certificate, active-set polish), in plain host code.  They make no device call and work in a
+ * process that never touches a GPU.  Same descriptors and argument meaning as the device entry
+ * points, except that every batch pointer is a HOST pointer and the last argument is a thread
+ * count (<= 0: all hardware threads) instead of a stream.  nu = 2. */
+typedef struct carmpc_cpu_problem carmpc_cpu_problem;
+int carmpc_cpu_problem_create(const carmpc_model_desc* desc, carmpc_cpu_problem** out);   /* <-> carmpc_problem_create */
+void carmpc_cpu_problem_destroy(carmpc_cpu_problem* prob);
+int carmpc_cpu_problem_info(const carmpc_cpu_problem* prob, int32_t* n, int32_t* p, int32_t* npre, int32_t* nx,
+                            int32_t* N);
+int carmpc_cpu_problem_set_disturbance(carmpc_cpu_problem* prob, const double* Bd /* NX */);
+/* MPCStateFB.step / MPCOutputFB.step QP (mpc.py:318-335, 461-478) for `batch` states. */
+int carmpc_cpu_solve_batch(const carmpc_cpu_problem* prob, int64_t batch, const double* x0, const double* xref,
+                           double* u_out, int32_t* status, int32_t* iters, const carmpc_settings* settings,
+                           int32_t threads);
+/* MPCOutputFBWithDisturbance.step QP (mpc.py:630-653): w = w0 - E x0 - Ed d_b. */
+int carmpc_cpu_solve_batch_dist(const carmpc_cpu_problem* prob, int64_t batch, const double* x0, const double* xref,
+                                const double* dist, double* u_out, int32_t* status, int32_t* iters,
+                                const carmpc_settings* settings, int32_t threads);
+
 /* Canonical per-iteration flop count of the dense condensed IPM
  * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);

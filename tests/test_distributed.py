@@ -1,18 +1,18 @@
 """N>1 path of bench.py on CPU: world_size-2 gloo over 127.0.0.1.
 
-The path shards (independent QP instances): every rank draws its own shard of the
-config-5 batch, solves it with no data-path collective, and the only exchange is the
-MAX over ranks of the wall time.  Here the solve is the oracle (test infrastructure);
-on the GPU box the same code path runs the HIP kernel."""
+The path shards (independent QP instances): every rank draws its own shard of the batch, solves
+it with no data-path collective, and the only exchanges are the barrier and the MAX over ranks
+of the wall time (gloo, host tensors).  The test runs bench.run -- the very control flow the
+driver launches with torch.distributed.run -- with the library's CPU QP path as the backend
+(--backend cpu); on a GPU box the same flow drives the HIP kernels."""
+import json
 import os
 import socket
 
 import numpy as np
-import pytest
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import REPO, TERMINAL_SETS
+from conftest import REPO
 
 
 def _free_port():
@@ -23,46 +23,57 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, argv):
     import sys
-    import time
-    import torch
     sys.path.insert(0, REPO)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="2")
     import bench
-    from oracle import assembly as oa
-    from oracle.cpu import CpuProblem
-    goals = [oa.ENVIRONMENTS[n][2] for n in bench.ENVS]
+    out = bench.run(bench.parse_args(argv))
+    goals = [[30, 1.5, 0, 0], [29.9, -1.5, 0, 0], [30, 1.5, 0, 0]]
     X, env, offsets = bench.sample_shard(rank, 240, goals)
-    t0 = time.perf_counter()
-    stats = []
-    for j, name in enumerate(bench.ENVS):
-        cp = CpuProblem(oa.build(name, 20, terminal_set_dir=TERMINAL_SETS))
-        _, st, _ = cp.solve(X[offsets[j]:offsets[j + 1]], threads=1)
-        stats.append(np.bincount(st, minlength=4))
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tot = torch.tensor(np.sum(stats, axis=0), dtype=torch.int64)
-    dist.all_reduce(tot)
-    q.put((rank, X[:3].copy(), env.tolist(), offsets.tolist(), float(t.item()), tot.tolist()))
-    dist.destroy_process_group()
+    q.put((rank, out, X[:3].copy(), env.tolist(), offsets.tolist()))
 
 
-def test_two_rank_sharding_gloo():
+def _run_world(world, argv):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, argv)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in procs])
+    res = sorted([q.get(timeout=400) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, x0, e0, o0, t0, s0), (r1, x1, e1, o1, t1, s1) = res
+    return res
+
+
+def test_bench_two_rank_flow_gloo():
+    argv = ["--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "cpu", "--per-gpu", "240", "--cpu-threads", "2",
+            "--cpu-sample", "96"]
+    (r0, out0, x0, e0, o0), (r1, out1, x1, e1, o1) = _run_world(2, argv)
+    assert out1 is None and out0 is not None            # rank 0 alone reports
+    json.dumps(out0)                                    # one JSON-serialisable line
+    assert out0["n_gpus"] == 2 and out0["steps"] == 2 and out0["warmup"] == 1 and out0["scaling"] == "weak"
+    assert out0["config"]["global_batch"] == 480 and out0["config"]["per_gpu_batch"] == 240
+    # value = instances of all ranks / max-over-ranks wall time
+    assert abs(out0["value"] - 480 * 2 / (out0["ms_per_step"] * 2e-3)) <= 1e-3 * out0["value"]
+    ss = out0["status_split"]
+    assert sum(ss.values()) == 240 and ss["max_iter"] == 0 and ss["numerical"] == 0 and ss["optimal"] > 100
+    # the CPU baseline and the iteration reference come from the oracle on rank 0 at any world size
+    cb = out0["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["single_thread"]["value"] > 0 and cb["cpu_model"]
+    assert cb["product_cpu_path"]["value"] > 0
     assert not np.allclose(x0, x1)                      # independent shards
     assert e0 == sorted(e0) and e1 == sorted(e1)        # grouped by environment
     assert o0[-1] == 240 and o1[-1] == 240
-    assert t0 == t1                                     # max-over-ranks timing agrees
-    assert s0 == s1 and sum(s0) == 480 and s0[2] == 0   # every instance certified
+
+
+def test_bench_single_rank_config4_flow_on_cpu():
+    """The OutputFB workload (observer + QP) through the same flow, one rank."""
+    import bench
+    out = bench.run(bench.parse_args(["--steps", "1", "--warmup", "0", "--backend", "cpu", "--workload", "config4",
+                                      "--per-gpu", "96", "--cpu-threads", "2", "--cpu-sample", "48"]))
+    assert out["config"]["workload"].startswith("config4") and out["config"]["step"].startswith("observer")
+    assert sum(out["status_split"].values()) == 96 and out["status_split"]["optimal"] > 10

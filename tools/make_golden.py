@@ -235,6 +235,29 @@ def main():
     np.savez(os.path.join(OUT, "closed_loop_statefb.npz"), states=np.array(traj), inputs=np.array(inputs))
     print("closed loop steps", len(traj), "final", traj[-1])
     meta["closed_loop_steps"] = len(traj)
+
+    # the plumbing configuration: the same runner on RoadEnv with N = 10.  The example's start
+    # [5, -1.5, 0.1, 0] is infeasible at N = 10 (the reference raises at step 0), so the trace
+    # starts at [22, 0, 0, 3]; it runs to the runner's time limit (i > 30 / DT_SIMULATION).
+    asm = oa.build("RoadEnv", 10, terminal_set_dir=os.path.join(REF, "terminal_sets"))
+    assert oq.solve_instance(asm, np.array([5, -1.5, 0.1, 0]))["status"] == oq.STATUS_INFEASIBLE
+    sim = ref_sim.CarSimulator(dt=ref_cfg.DT_SIMULATION)
+    sim.reset(np.array([22.0, 0.0, 0.0, 3.0]))
+    u = [0, 0]
+    traj, inputs = [], []
+    for i in range(1000):
+        sim.step(u)
+        traj.append(sim.state.copy())
+        if i % ref_cfg.STEPS_UPDATE == 0:
+            r = oq.solve_instance(asm, sim.state)
+            assert r["status"] == 0 and r["certified"]
+            u = r["u_exact"][:2]
+            inputs.append(u.copy())
+        if np.all(np.abs(sim.state - asm.goal) <= 1e-1) or i > 30 / ref_cfg.DT_SIMULATION:
+            break
+    np.savez(os.path.join(OUT, "closed_loop_statefb_RoadEnv_N10.npz"), states=np.array(traj), inputs=np.array(inputs))
+    print("RoadEnv N=10 closed loop steps", len(traj), "final", traj[-1])
+    meta["closed_loop_steps_RoadEnv_N10"] = len(traj)
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
 
