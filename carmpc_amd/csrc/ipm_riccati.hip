@@ -90,7 +90,7 @@ constexpr int REC = 20;   // doubles per stage record (160 B)
 //   [12..15] b^x_{t+1} | y_{t+1} | gz_t [12..13], hs_t [14..15]
 //   [16..17] b^u_t | v_t
 //   [18..19] Db_t | kappa_t
-constexpr int O_K = 0, O_CH = 8, O_BX = 12, O_BU = 16, O_DB = 18;
+constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
 
 constexpr double POLISH_MU = 1e-6;
 constexpr double POLISH_DELTA = 1e-10;
@@ -575,6 +575,216 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         wb();
     };
 
+
+    // ---- stage recursions on the matrix cores (shared-model problems) -------------------
+    // v_mfma_f64_4x4x4f64 multiplies four independent 4x4 blocks per wavefront; block b lives in
+    // lanes 16 r + 4 b + c (r, c = 0..3), and with X^ the 4x4 matrix whose entry (r, c) is the
+    // value lane (r, c) holds in register X, the instruction computes  D^ = A^' B^ + C^
+    // (operand A enters transposed; the neg modifier negates an operand for free).  In the
+    // recursion phases block b therefore works on QP group b with ONE matrix entry per lane --
+    // P, K, the 2x2 pivots are single registers -- instead of every lane of a group repeating the
+    // whole 4x4 recursion; vectors are 4x4 operands whose columns all hold the vector (the adjoint
+    // pass carries psiZ / psiH in columns 0 / 1).  Stage data is exchanged with the row phases
+    // through the same LDS records.  The passes are straight-line code without exec masking:
+    //   * all four blocks always compute (MFMA needs the whole wave); a block whose group sits out
+    //     a pass only overwrites record fields that are dead until the group's next trip;
+    //   * structural zeros (rows 2-3 of K, of b^u, ...) are loaded from slot 11 of each record,
+    //     which always holds 0.0, and lanes whose result is a structural zero store it there;
+    //   * lanes that hold copies of one value (the columns of a vector) all store it.
+    const int mb = (lane >> 2) & 3, mr = lane >> 4, mc = lane & 3;
+    double* recm = wv.recbuf + mb * (N * REC);
+    auto mm = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0); };
+    auto mm_na = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1); };
+    const bool m_top = mr < 2, m_left = mc < 2;
+    const int oW = sym10(mr, mc);                              // W^, P^ entry in the packed 10-vector
+    const int oK = m_top ? O_K + 4 * mr + mc : O_ZERO;         // K^ (rows 0-1)
+    const int oKT = m_left ? O_K + 4 * mc + mr : O_ZERO;       // K'^ (columns 0-1)
+    const int oLam = m_left ? 4 * mc + mr : O_ZERO;            // [lamZ lamH 0 0]
+    const int oGH = (m_top && m_left) ? 12 + 2 * mc + mr : O_ZERO;   // gz, hs
+    const int oBUt = m_top ? O_BU + mr : O_ZERO;               // b^u / v in rows 0-1
+    const int oBU1 = mr == 1 ? O_BU : O_ZERO;                  // b^u_0 in row 1 (for E b^u)
+    const int oKPt = m_top ? O_DB + mr : O_ZERO;               // kappa in rows 0-1
+    const int oDrow = O_CH + (mr == 0 ? 1 : 2);                // 1/p0 in row 0, 1/p1 below
+    double cA = 0.0, cAT = 0.0, cBp = 0.0, cBpT = 0.0, cB0r = 0.0, cB1r = 0.0, cB0m1 = 0.0, cQ = 0.0, cPt = 0.0;
+    if constexpr (!HET) {
+        cA = MT.A[mr * 4 + mc];                       // A^
+        cAT = MT.A[mc * 4 + mr];                      // (A')^
+        cBp = m_left ? MT.B[mr * 2 + mc] : 0.0;       // [B 0 0]^
+        cBpT = m_top ? MT.B[mc * 2 + mr] : 0.0;       // [B 0 0]'^
+        cB0r = MT.B[mr * 2];                          // column 0 of B in every column
+        cB1r = MT.B[mr * 2 + 1];                      // column 1 of B in every column
+        cB0m1 = mc == 1 ? cB0r : 0.0;
+        cQ = MT.Q[mr * 4 + mc];
+        cPt = MT.P[mr * 4 + mc];
+    }
+    const double k10 = (mr == 1 && mc == 0) ? 1.0 : 0.0, kd = (mr == mc && m_top) ? 1.0 : 0.0;
+    // One wave per SIMD leaves nothing to hide an LDS round trip (~70 cycles) or an MFMA result
+    // (28 cycles to a dependent MFMA, 16 cycles of pipe each) behind, so the passes are software
+    // pipelined by hand: stage t's record fields are read kPre stages ahead, side products and
+    // stores trail the recursion by a stage, and a scheduling barrier closes every stage -- without
+    // it the compiler sinks the stores (nothing waits for them) and, since it cannot rule out an
+    // alias between lane-dependent LDS offsets, every later load sinks behind them, back onto the
+    // critical path.  The loops are fully unrolled; staged values sit in registers.
+    constexpr int kPre = 3;
+    auto stage_fence = [] { __builtin_amdgcn_sched_barrier(0); };
+    // adjoint pass: psi_k = lam_k + A'psi_{k+1} for lamZ (column 0) and lamH (column 1);
+    // gz_t, hs_t = B'psi_{t+1} -> rec[t][12..15]
+    auto adjoint_mm = [&]() {
+        wb();
+        double lam[N], psi[N + 1], gh[N];
+        psi[N] = 0.0;
+#pragma unroll
+        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) lam[t] = recm[t * REC + oLam];
+        stage_fence();
+#pragma unroll
+        for (int t = N - 1; t >= -2; --t) {
+            if (t - kPre >= 0) lam[t - kPre] = recm[(t - kPre) * REC + oLam];
+            if (t >= 0) psi[t] = mm(cA, psi[t + 1], lam[t]);
+            if (t + 1 >= 0 && t + 1 < N) gh[t + 1] = mm(cBp, psi[t + 1], 0.0);
+            if (t + 2 < N) recm[(t + 2) * REC + oGH] = gh[t + 2];
+            stage_fence();
+        }
+        wb();
+    };
+    // Riccati factorization (W_k, Db_t in rec) fused with the backward pass of the first
+    // right-hand side.  Re_t = R + Db_t + B'PB = L D^{-1} L' with L = [[1, 0], [l, 1]] and
+    // D = diag(1/p0, 1/p1), guarded like the Cholesky it replaces (a non-positive pivot becomes
+    // 1e128), and Re_t^{-1} = E'D E with E = L^{-1} is applied in that factored form -- E F first,
+    // then D, then E' -- never as an explicit inverse: when B'PB is nearly singular the rows of
+    // F = B'PA are nearly dependent, and only the factored form subtracts them before scaling (an
+    // explicit inverse stalled the IPM on such instances).  The three entries of Re_t come out of
+    // MFMAs with B's columns replicated, so every lane of the block holds them (no cross-lane
+    // broadcast).  K_t -> rec[t][0..7], (l, 1/p0, 1/p1) -> rec[t][8..10], kappa_t -> rec[t][18..19]
+    auto factor_mm = [&]() {
+        wb();
+        struct In { double db0, db1, buT, bu01, Wt, bxv; };
+        struct Out { double En, Z, zg, l, drow; };
+        In in[N];
+        Out o[N];
+        auto load = [&](int t) {
+            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
+            in[t].db0 = recm[r + O_DB];
+            in[t].db1 = recm[r + O_DB + 1];
+            in[t].buT = recm[r + oBUt];
+            in[t].bu01 = recm[r + oBU1];
+            in[t].Wt = recm[rp + oW];
+            in[t].bxv = recm[rp + O_BX + mr];
+        };
+        double Pm = cPt + recm[(N - 1) * REC + oW];
+        double pv = recm[(N - 1) * REC + O_BX + mr];
+#pragma unroll
+        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) load(t);
+        stage_fence();
+#pragma unroll
+        for (int t = N - 1; t >= -1; --t) {
+            if (t - kPre >= 0) load(t - kPre);
+            if (t >= 0) {
+                const double T = mm(Pm, cA, 0.0);             // P A
+                const double PB0 = mm(Pm, cB0r, 0.0);         // every column: P b0
+                const double PB1 = mm(Pm, cB1r, 0.0);         // every column: P b1
+                const double re00 = mm(cB0r, PB0, MT.R[0] + in[t].db0);   // every entry: (R + Db + B'PB)_00
+                const double re10 = mm(cB1r, PB0, MT.R[2]);
+                const double re11 = mm(cB1r, PB1, MT.R[3] + in[t].db1);
+                const double apT = mm(cA, T, cQ + in[t].Wt);  // Qbar_t + W_t + A'(P A)
+                const double app = mm(cA, pv, in[t].bxv);     // b^x_t + A'p
+                const double p0 = re00 > 0.0 ? re00 : 1e128;
+                const double det = fma(p0, re11, -(re10 * re10));   // p0 p1
+                const double r0 = frcp(p0);
+                const double rd = frcp(det > 0.0 ? det : 1.0);
+                const double ip1 = det > 0.0 ? p0 * rd : 1e-128;    // 1/p1, p1 = re11 - re10^2/p0
+                const double l = re10 * r0;
+                const double drow = mr == 0 ? r0 : ip1;
+                const double Xl = fma(-l, cB0m1, cBp);              // [B 0 0] E'
+                const double Y = mm(Xl, T, 0.0);                    // rows 0-1: E B'PA
+                const double yg = mm(Xl, pv, fma(-l, in[t].bu01, in[t].buT));   // rows 0-1: E (b^u + B'p)
+                o[t].En = fma(-l, k10, kd);                         // E (2x2 block)
+                o[t].Z = Y * drow;
+                o[t].zg = yg * drow;
+                o[t].l = l;
+                o[t].drow = drow;
+                // P_t = Qbar_t + W_t + A'(P A) - F'K with F'K = Y'Z;  p_t = b^x_t + A'p - K'g, K'g = Y'zg
+                Pm = mm_na(Y, o[t].Z, apT);
+                pv = mm_na(Y, o[t].zg, app);
+            }
+            if (t + 1 < N) {   // the previous stage's gain, multiplier and factor, off the recursion's path
+                const int r = (t + 1) * REC;
+                recm[r + oK] = mm(o[t + 1].En, o[t + 1].Z, 0.0);       // rows 0-1: E'D E F = Re^{-1} F
+                recm[r + oKPt] = mm(o[t + 1].En, o[t + 1].zg, 0.0);    // rows 0-1: Re^{-1} g
+                recm[r + O_CH] = o[t + 1].l;
+                recm[r + oDrow] = o[t + 1].drow;
+            }
+            stage_fence();
+        }
+        wb();
+    };
+    // backward linear pass with the stored factor: kappa_t = Re_t^{-1}(b^u_t + B'p_{t+1}) in the
+    // factored form above, p_t = b^x_t + A'p_{t+1} - K_t'g_t
+    auto back_mm = [&]() {
+        wb();
+        struct In { double buT, bu01, l, drow, K, bxv; };
+        In in[N];
+        double En[N], zg[N];
+        auto load = [&](int t) {
+            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
+            in[t].buT = recm[r + oBUt];
+            in[t].bu01 = recm[r + oBU1];
+            in[t].l = recm[r + O_CH];
+            in[t].drow = recm[r + oDrow];
+            in[t].K = recm[r + oK];
+            in[t].bxv = recm[rp + O_BX + mr];
+        };
+        double pv = recm[(N - 1) * REC + O_BX + mr];
+#pragma unroll
+        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) load(t);
+        stage_fence();
+#pragma unroll
+        for (int t = N - 1; t >= -1; --t) {
+            if (t - kPre >= 0) load(t - kPre);
+            if (t >= 0) {
+                const double l = in[t].l;
+                const double g = mm(cBp, pv, in[t].buT);
+                const double app = mm(cA, pv, in[t].bxv);
+                const double yg = mm(fma(-l, cB0m1, cBp), pv, fma(-l, in[t].bu01, in[t].buT));
+                En[t] = fma(-l, k10, kd);
+                if (t >= 1) pv = mm_na(in[t].K, g, app);
+                zg[t] = yg * in[t].drow;
+            }
+            if (t + 1 < N) recm[(t + 1) * REC + oKPt] = mm(En[t + 1], zg[t + 1], 0.0);
+            stage_fence();
+        }
+        wb();
+    };
+    // forward pass: v_t = kappa_t - K_t y_t -> rec[t][16..17]; y_{t+1} = A y_t + B v_t -> rec[t][12..15]
+    auto forward_mm = [&]() {
+        wb();
+        double KT[N], kp[N], y[N + 1], v[N];
+        y[0] = 0.0;
+#pragma unroll
+        for (int t = 0; t < N && t < kPre; ++t) {
+            KT[t] = recm[t * REC + oKT];
+            kp[t] = recm[t * REC + oKPt];
+        }
+        stage_fence();
+#pragma unroll
+        for (int t = 0; t <= N; ++t) {
+            if (t + kPre < N) {
+                KT[t + kPre] = recm[(t + kPre) * REC + oKT];
+                kp[t + kPre] = recm[(t + kPre) * REC + oKPt];
+            }
+            if (t < N) {
+                v[t] = mm_na(KT[t], y[t], kp[t]);              // rows 0-1: kappa - K y
+                const double ay = mm(cAT, y[t], 0.0);          // A y
+                y[t + 1] = mm(cBpT, v[t], ay);                 // + B v
+            }
+            if (t >= 1) {
+                recm[(t - 1) * REC + O_BX + mr] = y[t];
+                recm[(t - 1) * REC + oBUt] = v[t - 1];
+            }
+            stage_fence();
+        }
+        wb();
+    };
+
     // Each group claims its next instance from the launch's counter (S.claim, one atomic per
     // instance by the group's lane 0) at the first trip after finishing one, so the 4 groups
     // of a wave never wait for the slowest instance and no group is left with a heavier static
@@ -620,6 +830,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         RT_MARK(11);
         if (live && fresh) {
             fresh = false;
+            if constexpr (!HET) {   // slot 11 of every record is the matrix-core passes' source of structural zeros
+                for (int t = j; t < N; t += G16) rec[t * REC + O_ZERO] = 0.0;
+            }
             // this instance's data (HET) / the launch's problem
             const double *Ipw = P.pre_w0, *IpE = P.pre_E, *Irw = P.r_w0, *IrE = P.r_E, *Ihq = P.hq;
             if constexpr (HET) {
@@ -785,9 +998,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 umax = row_max(umax);
                 wz = row_sum(wz);
                 wzabs = row_sum(wzabs);
-                // B1: psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1}
+            }
+            // B1 (per-instance models): psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1},
+            // redundantly in the 16 lanes of the group
+            auto adjoint_scalar = [&]() {
                 wb();
-                {
                     double pz[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};
                     double lzv[4], lhv[4];
                     rd4((N - 1) * REC + 0, lzv);
@@ -834,8 +1049,15 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
 #pragma unroll
                         for (int a = 0; a < 4; ++a) { lzv[a] = nlz[a]; lhv[a] = nlh[a]; }
                     }
-                }
                 wb();
+            };
+            // B1: psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1}
+            if constexpr (HET) {
+                if (active) adjoint_scalar();
+            } else {
+                adjoint_mm();
+            }
+            if (active) {
                 RT_MARK(2);
                 double rdn = 0.0, hun = 0.0, gzn = 0.0;
 #pragma unroll
@@ -847,6 +1069,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     const double gzv[2] = {gz0, gz1}, hsv[2] = {hs0, hs1};
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
+                        if constexpr (!HET) {   // box-Farkas sums over the owned inputs (summed over the group below)
+                            const double lb = sh.lb[2 * (kseg[sg] - 1) + c], ub = sh.ub[2 * (kseg[sg] - 1) + c];
+                            if (own[sg]) {
+                                lo += fmin(gzv[c] * lb, gzv[c] * ub);
+                                scf = fma(fabs(gzv[c]), fmax(fabs(lb), fabs(ub)), scf);
+                            }
+                        }
                         const double hu = hsv[c] + M.Rmul(c, BX(F_U, sg, 0), BX(F_U, sg, 1));
                         const double gzb = gzv[c] + (boxed ? BX(F_ZU, sg, c) - BX(F_ZL, sg, c) : 0.0);
                         const double rd = hu + BX(F_Q, sg, c) + gzb;
@@ -861,6 +1090,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 rdn = row_max(rdn);
                 hun = row_max(hun);
                 gzn = row_max(gzn);
+                if constexpr (!HET) {
+                    lo = row_sum(lo);
+                    scf = row_sum(scf);
+                }
                 const double pscale = fmax(bnorm, 1.0 + fmax(gun, umax));
                 const double dscale = fmax(qnorm, 1.0 + fmax(hun, gzn));
                 int done = -1;
@@ -965,9 +1198,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     }
                 }
                 RT_MARK(4);
-                factor_and_back();
-                RT_MARK(5);
+                if constexpr (HET) factor_and_back();
             }
+            if constexpr (!HET) factor_mm();
+            RT_MARK(5);
             // ================= solves =================
             // fully unrolled: k is a constant in every branch below (precise register lifetimes)
             // the refinement solve (k = 2 of a normal trip) only once mu <= REFINE_MU; before
@@ -978,9 +1212,18 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                 if (k == 3 && !any_polish) break;
                 const bool run = active && (polish || k < 3);
                 const bool solve = run && (polish || k != 2 || refine);
-                if (k > 0 && solve) back_linear();
-                RT_MARK(6);
-                if (solve) forward();
+                if constexpr (HET) {
+                    if (k > 0 && solve) back_linear();
+                    RT_MARK(6);
+                    if (solve) forward();
+                } else {
+                    // the matrix-core passes run for the whole wave; groups that sit out only skip the stores
+                    if (__any(solve)) {
+                        if (k > 0) back_mm();
+                        RT_MARK(6);
+                        forward_mm();
+                    }
+                }
                 RT_MARK(7);
                 if (!run) continue;
                 double dy[2][4], dv[2][2];
@@ -1350,6 +1593,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
                     polish_failed = false;
                     ++it;
                     RT_MARK(10);
+                }
+            }
+            if constexpr (!HET) {
+                // the polish's pair check borrows the record buffer of the whole wave: restore the zero slots
+                if (any_polish && P.r_partner) {
+                    wb();
+                    for (int t = j; t < N; t += G16) rec[t * REC + O_ZERO] = 0.0;
+                    wb();
                 }
             }
         }

@@ -26,7 +26,7 @@ PHASES = ["init", "residual rows", "adjoint pass", "decisions", "factor rows", "
 def main():
     kernel = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     dev = torch.device("cuda", 0)
-    ctrls = bench.build_problems(dev)
+    ctrls = bench.build_controllers(bench.ENVS, 20, dev)
     probs = [c.qp for c in ctrls]
     X, env, offsets = bench.sample_shard(0, bench.PER_GPU, [c.goal for c in ctrls])
     Xd = torch.as_tensor(X).to(dev)
