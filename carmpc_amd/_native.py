@@ -28,7 +28,7 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
            "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
            "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
-           "carmpc_hetero_get", "carmpc_set_serial_segments", "carmpc_solve_batch_noalloc",
+           "carmpc_hetero_get", "carmpc_solve_batch_noalloc",
            "carmpc_problem_set_observer", "carmpc_cpu_problem_create", "carmpc_cpu_problem_destroy",
            "carmpc_cpu_problem_info", "carmpc_cpu_problem_set_disturbance", "carmpc_cpu_solve_batch",
            "carmpc_cpu_solve_batch_dist")
@@ -126,7 +126,6 @@ def load():
         "carmpc_hetero_destroy": ([vp], None),
         "carmpc_hetero_linearize": ([vp, vp, vp, vp], ctypes.c_int),
         "carmpc_hetero_solve": ([vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
-        "carmpc_set_serial_segments": ([i32], None),
         "carmpc_hetero_get": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "carmpc_closed_loop_batch": ([vp, i64, ctypes.POINTER(LoopDesc), vp, vp, vp, vp, vp, vp, vp, i32,
                                       ctypes.POINTER(Settings), vp], ctypes.c_int),

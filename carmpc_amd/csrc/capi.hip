@@ -107,31 +107,6 @@ struct carmpc_hetero {
 };
 
 namespace {
-// side streams of carmpc_solve_segments, one set per (thread, device)
-struct SideStreams {
-    static constexpr int kN = 4;
-    hipStream_t s[kN];
-    hipEvent_t fork, join[kN];
-};
-bool g_serial_segments = false;
-SideStreams* side_streams() {
-    thread_local SideStreams* per_dev[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    if (!per_dev[dev]) {
-        auto* ss = new SideStreams();
-        for (int i = 0; i < SideStreams::kN; ++i) {
-            if (hipStreamCreateWithFlags(&ss->s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
-            if (hipEventCreateWithFlags(&ss->join[i], hipEventDisableTiming) != hipSuccess) return nullptr;
-        }
-        if (hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-        per_dev[dev] = ss;
-    }
-    return per_dev[dev];
-}
-}  // namespace
-
-namespace {
 thread_local std::string g_err;
 
 int fail(int code, const std::string& msg) {
@@ -805,64 +780,60 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
                           int32_t* iters, const carmpc_settings* settings, hipStream_t stream) {
     if (!probs || !offsets || nprobs < 0) return fail(CARMPC_EINVAL, "null argument");
     const Settings s = make_settings(settings);
-    int live = 0;
+    std::vector<int> live;
     for (int j = 0; j < nprobs; ++j) {
         const int64_t b0 = offsets[j], b1 = offsets[j + 1];
-        if (b1 < b0) return fail(CARMPC_EINVAL, "offsets must be non-decreasing");
+        if (b0 < 0 || b1 < b0) return fail(CARMPC_EINVAL, "offsets must be non-negative and non-decreasing");
         if (b1 == b0) continue;
         if (!probs[j]) return fail(CARMPC_EINVAL, "null problem in segment list");
         if (ld_u < probs[j]->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
-        ++live;
+        live.push_back(j);
     }
-    // Several segments: fork them onto side streams so a launch's tail (groups finishing their
-    // last instances) overlaps the next segment's start, then join back into `stream`.
-    // The claim counters of all segments are zeroed by one fill on `stream` before the fork: a
-    // fill on a side stream would queue behind the first segment's kernel (which holds every CU)
-    // and hold its own segment back until that kernel drains (seen in the v10 kernel trace).
-    SideStreams* side = nullptr;
+    if (live.empty()) return CARMPC_OK;
+    if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
+    // Runs of consecutive segments that share one instantiation of the grouped Riccati kernel go out
+    // as ONE launch (ipm_riccati_segs_kernel: workgroups move from a drained segment to the others),
+    // so no segment ends with its own launch tail; anything else is launched per problem.  All
+    // launches are queued on `stream`, one claim counter per segment from one stream-ordered block.
+    auto ric_ok = [&](int j) { return (s.kernel == 0 || s.kernel == 7) && probs[j]->dev.ric != 0; };
     unsigned* counters = nullptr;
-    constexpr int kCounterStride = 16;   // one 64-B line per segment counter
-    if (live > 1 && !g_serial_segments) {
-        side = side_streams();
-        if (!side) return hipfail(hipGetLastError(), "side streams");
-        const size_t bytes = sizeof(unsigned) * kCounterStride * live;
-        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&counters), bytes, stream), "segment counters");
-        HIP_TRY(launch_zero_u32(counters, kCounterStride * live, stream), "zero segment counters");
-        HIP_TRY(hipEventRecord(side->fork, stream), "fork event");
-    }
-    int k = 0, rc = CARMPC_OK;
-    for (int j = 0; j < nprobs; ++j) {
-        const int64_t b0 = offsets[j], b1 = offsets[j + 1];
-        if (b1 == b0) continue;
-        const carmpc_problem* P = probs[j];
-        hipStream_t sj = stream;
-        if (side) {
-            sj = side->s[k % SideStreams::kN];
-            HIP_TRY(hipStreamWaitEvent(sj, side->fork, 0), "side stream wait");
-        }
+    const size_t ncount = (size_t)kRicClaimStride * live.size();
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&counters), sizeof(unsigned) * ncount, stream), "segment counters");
+    int rc = CARMPC_OK;
+    hipError_t e = launch_zero_u32(counters, (int)ncount, stream);
+    if (e != hipSuccess) rc = hipfail(e, "zero segment counters");
+    for (size_t i = 0; i < live.size() && rc == CARMPC_OK;) {
+        size_t i1 = i + 1;
+        if (ric_ok(live[i]))
+            while (i1 < live.size() && i1 - i < (size_t)kRicMaxSeg && live[i1] == live[i1 - 1] + 1 && ric_ok(live[i1]) &&
+                   probs[live[i1]]->dev.N == probs[live[i]]->dev.N && probs[live[i1]]->dev.ric == probs[live[i]]->dev.ric)
+                ++i1;
         Settings sk = s;
-        if (counters) sk.claim = counters + kCounterStride * k;
-        ++k;
+        sk.claim = counters + kRicClaimStride * i;
         int unsupported = 0;
-        hipError_t e = launch_solve(P->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u,
-                                    ld_u, status + b0, iters ? iters + b0 : nullptr, sk, sj, &unsupported);
-        if (unsupported || e != hipSuccess) {   // join what was queued, then report
-            rc = unsupported ? fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size")
-                             : hipfail(e, "segment launch");
-            break;
+        if (i1 - i >= 2) {
+            RicSegs T{};
+            T.nseg = (int)(i1 - i);
+            for (size_t k = i; k < i1; ++k) {
+                T.off[k - i] = offsets[live[k]];
+                T.P[k - i] = probs[live[k]]->dev;
+            }
+            T.off[i1 - i] = offsets[live[i1 - 1] + 1];
+            e = launch_riccati_segs(T, x0, xref, u_out, ld_u, status, iters, sk, stream, &unsupported);
+        } else {
+            const int j = live[i];
+            const int64_t b0 = offsets[j], b1 = offsets[j + 1];
+            e = launch_solve(probs[j]->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u, ld_u,
+                             status + b0, iters ? iters + b0 : nullptr, sk, stream, &unsupported);
         }
+        if (unsupported) rc = fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
+        else if (e != hipSuccess) rc = hipfail(e, "segment launch");
+        i = i1;
     }
-    if (side) {
-        for (int i = 0; i < k && i < SideStreams::kN; ++i) {
-            HIP_TRY(hipEventRecord(side->join[i], side->s[i]), "join event");
-            HIP_TRY(hipStreamWaitEvent(stream, side->join[i], 0), "join wait");
-        }
-        HIP_TRY(hipFreeAsync(counters, stream), "free segment counters");
-    }
+    e = hipFreeAsync(counters, stream);
+    if (rc == CARMPC_OK && e != hipSuccess) rc = hipfail(e, "free segment counters");
     return rc;
 }
-
-void carmpc_set_serial_segments(int32_t serial) { g_serial_segments = serial != 0; }
 
 int carmpc_problem_set_disturbance(carmpc_problem* P, const double* Bd) {
     if (!P || !Bd) return fail(CARMPC_EINVAL, "null argument");

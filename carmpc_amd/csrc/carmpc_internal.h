@@ -271,6 +271,17 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
                           double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
                           const Settings& s, hipStream_t stream, int* unsupported, bool het = false);
 
+// Several problems in one Riccati launch (carmpc_solve_segments): descriptors by value in the
+// kernel arguments, segment j = instances [off[j], off[j+1]), claim counter j at claim + 16 j.
+constexpr int kRicMaxSeg = 4, kRicClaimStride = 16;
+struct RicSegs {
+    int32_t nseg;
+    int64_t off[kRicMaxSeg + 1];
+    DevProblem P[kRicMaxSeg];
+};
+hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
+                               int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported);
+
 // Stage-structured kernel (ipm_staged.hip).
 constexpr int kStagedMaxRS = 4;
 bool staged_supported_N(int N);

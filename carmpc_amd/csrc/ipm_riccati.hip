@@ -21,6 +21,7 @@
 #include "carmpc_internal.h"
 #include "lanes.h"
 
+#include <algorithm>
 #include <type_traits>
 
 #include <hip/hip_runtime.h>
@@ -69,6 +70,10 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #define RIC_WRITER (j == 0)
 #else
 #define RIC_WRITER true
+#endif
+// Stages of read-ahead of the matrix-core passes (see the comment at kPre).
+#ifndef CARMPC_RIC_KPRE
+#define CARMPC_RIC_KPRE 3
 #endif
 #ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
                                 // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
@@ -191,15 +196,43 @@ struct MtH {
 
 // HET: every instance has its own linearisation (hetero.hip): A, B, P, slot row norms, w0, E,
 // hq and x0-only rows come from the instance's slices; the row layout is the template's.
+// One launch serves up to kRicMaxSeg problems (instance segments, carmpc_solve_segments); a
+// single problem is the one-segment case.  The descriptors travel by value in the kernel arguments
+// (scalar loads), every segment has its own claim counter (S.claim + 16 seg), and the workgroups
+// are dealt to "home" segments in proportion to the instance counts.  A workgroup serves its home
+// segment until that counter runs out, then moves on round-robin to help with the others
+// (reloading the problem's slot tables), so the launch ends when every segment is drained -- no
+// per-problem launch tail, no side streams.
 template <int N, int WPB, class SP, bool HET = false>
-__global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int64_t batch, const double* __restrict__ x0,
-                                                               const double* __restrict__ xref, double* __restrict__ u_out,
-                                                               int64_t ld_u, int32_t* __restrict__ status_out,
-                                                               int32_t* __restrict__ iters_out, Settings S) {
+__global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const double* __restrict__ x0_all,
+                                                               const double* __restrict__ xref_all,
+                                                               double* __restrict__ u_all, int64_t ld_u,
+                                                               int32_t* __restrict__ status_all,
+                                                               int32_t* __restrict__ iters_all, Settings S_all) {
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
     constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
     __shared__ __attribute__((aligned(16))) RicWave<N> wscr[WPB];
+    const int nseg = T.nseg;
+    int home = 0;
+    if (nseg > 1) {
+        const int64_t first = T.off[0], total = T.off[nseg] - first;
+        const int64_t pos = first + (int64_t)blockIdx.x * total / gridDim.x;
+        while (home + 1 < nseg && pos >= T.off[home + 1]) ++home;
+    }
+    for (int kseg_i = 0; kseg_i < nseg; ++kseg_i) {
+    const int seg = nseg > 1 ? (home + kseg_i) % nseg : 0;
+    const DevProblem& P = T.P[seg];
+    const int64_t seg0 = T.off[seg], batch = T.off[seg + 1] - seg0;
+    const double* __restrict__ x0 = x0_all + seg0 * NX;
+    const double* __restrict__ xref = xref_all ? xref_all + seg0 * NX : nullptr;
+    double* __restrict__ u_out = u_all + seg0 * ld_u;
+    int32_t* __restrict__ status_out = status_all + seg0;
+    int32_t* __restrict__ iters_out = iters_all ? iters_all + seg0 : nullptr;
+    Settings S = S_all;
+    if (S.claim) S.claim += kRicClaimStride * seg;
+    if (kseg_i > 0) __syncthreads();   // every wave is done with the previous problem's tables
+    if (batch <= 0) continue;
     const StageMats& MT = P.mats;
     std::conditional_t<HET, MtH<SP>, const Mt<SP>> M{P.mats};
     int64_t hinst = 0;   // HET: the group's current instance (slice index)
@@ -625,7 +658,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
     // it the compiler sinks the stores (nothing waits for them) and, since it cannot rule out an
     // alias between lane-dependent LDS offsets, every later load sinks behind them, back onto the
     // critical path.  The loops are fully unrolled; staged values sit in registers.
-    constexpr int kPre = 3;
+    constexpr int kPre = CARMPC_RIC_KPRE;
     auto stage_fence = [] { __builtin_amdgcn_sched_barrier(0); };
     // adjoint pass: psi_k = lam_k + A'psi_{k+1} for lamZ (column 0) and lamH (column 1);
     // gz_t, hs_t = B'psi_{t+1} -> rec[t][12..15]
@@ -1606,11 +1639,51 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(DevProblem P, int
         }
     }
     RT_FLUSH();
+    }   // segments
 }
 
 }  // namespace
 
 bool riccati_supported_N(int N) { return N == 10 || N == 20; }
+
+namespace {
+// grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
+template <class Kern>
+hipError_t ric_launch(Kern kern, const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out,
+                      int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
+    constexpr int WPB = 4;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, WPB * 64, 0);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const int64_t per_block = (int64_t)WPB * 4;
+    int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, (total + per_block - 1) / per_block);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, T, x0, xref, u_out, ld_u, status, iters, s);
+    return hipGetLastError();
+}
+template <bool HET>
+hipError_t ric_dispatch(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
+                        int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
+    constexpr int WPB = 4;
+    const bool bike = T.P[0].ric == 2;
+    if (HET && !bike) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
+        *unsupported = 1;
+        return hipErrorInvalidValue;
+    }
+#define RIC_GO(NN, MODEL) ric_launch(ipm_riccati_kernel<NN, WPB, MODEL, HET>, T, total, x0, xref, u_out, ld_u, status, iters, s, stream)
+    switch (T.P[0].N) {
+        case 10: return bike ? RIC_GO(10, BicycleModel) : RIC_GO(10, DenseModel);
+        case 20: return bike ? RIC_GO(20, BicycleModel) : RIC_GO(20, DenseModel);
+        default: *unsupported = 1; return hipErrorInvalidValue;
+    }
+#undef RIC_GO
+}
+}  // namespace
 
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
                           int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
@@ -1621,45 +1694,35 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
-    constexpr int WPB = 4;
-    auto go = [&](auto kern) -> hipError_t {
-        int dev = 0, cus = 0, per_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, WPB * 64, 0);
-        if (e != hipSuccess) return e;
-        if (per_cu < 1) per_cu = 1;
-        const int64_t per_block = (int64_t)WPB * 4;
-        int64_t want = (batch + per_block - 1) / per_block;
-        int64_t grid = (int64_t)cus * per_cu;
-        if (want < grid) grid = want;
-        if (grid < 1) grid = 1;
-        // per-launch claim counter, stream-ordered (allocated, zeroed, freed on `stream`)
-        return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, P, batch, x0, xref, u_out, ld_u,
-                               status, iters, sc);
-            return hipGetLastError();
-        });
-    };
-    const bool bike = P.ric == 2;
-    if (het) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
-        if (!bike) {
+    RicSegs T{};
+    T.nseg = 1;
+    T.off[0] = 0;
+    T.off[1] = batch;
+    T.P[0] = P;
+    // per-launch claim counter, stream-ordered (allocated, zeroed, freed on `stream`)
+    return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
+        return het ? ric_dispatch<true>(T, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported)
+                   : ric_dispatch<false>(T, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported);
+    });
+}
+
+hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
+                               int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
+    *unsupported = 0;
+    static_assert(sizeof(RicSegs) + 6 * sizeof(void*) + sizeof(Settings) + 64 <= 4096, "kernel arguments exceed 4 KB");
+    const int nseg = T.nseg;
+    if (nseg < 1 || nseg > kRicMaxSeg || !s.claim) {
+        *unsupported = 1;
+        return hipErrorInvalidValue;
+    }
+    for (int j = 0; j < nseg; ++j)
+        if (!T.P[j].ric || T.P[j].N != T.P[0].N || T.P[j].ric != T.P[0].ric) {
             *unsupported = 1;
             return hipErrorInvalidValue;
         }
-        switch (P.N) {
-            case 10: return go(ipm_riccati_kernel<10, WPB, BicycleModel, true>);
-            case 20: return go(ipm_riccati_kernel<20, WPB, BicycleModel, true>);
-            default: *unsupported = 1; return hipErrorInvalidValue;
-        }
-    }
-    switch (P.N) {
-        case 10: return bike ? go(ipm_riccati_kernel<10, WPB, BicycleModel>) : go(ipm_riccati_kernel<10, WPB, DenseModel>);
-        case 20: return bike ? go(ipm_riccati_kernel<20, WPB, BicycleModel>) : go(ipm_riccati_kernel<20, WPB, DenseModel>);
-        default: *unsupported = 1; return hipErrorInvalidValue;
-    }
+    const int64_t total = T.off[nseg] - T.off[0];
+    if (total <= 0) return hipSuccess;
+    return ric_dispatch<false>(T, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
 }
 
 }  // namespace carmpc

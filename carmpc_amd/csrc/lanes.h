@@ -39,7 +39,11 @@ __device__ __forceinline__ double row_min(double v) { return row_reduce<OpMin>(v
 __device__ __forceinline__ double frcp(double b) {
     double r = __builtin_amdgcn_rcp(b);
     r = fma(fma(-b, r, 1.0), r, r);
+#ifdef CARMPC_FRCP_NR1   // A/B: v_rcp_f64 is good to ~2^-25, one step leaves <= 11 ulp
+    return r;
+#else
     return fma(fma(-b, r, 1.0), r, r);
+#endif
 }
 __device__ __forceinline__ double frsq(double a) {
     double r = __builtin_amdgcn_rsq(a);

@@ -387,7 +387,8 @@ class CpuQPProblem:
 def solve_segments(problems: list, offsets, x0: torch.Tensor, xref: torch.Tensor | None = None,
                    settings: SolverSettings | None = None, stream=None, out: tuple | None = None):
     """Instances grouped by problem: rows [offsets[j], offsets[j+1]) use problems[j]; one call
-    solves all segments (stream-ordered on ``stream``).  ``xref`` is B x 4 or 1 x 4;
+    solves all segments, in one kernel launch where the problems share a kernel instantiation
+    (stream-ordered on ``stream``).  ``xref`` is B x 4 or 1 x 4;
     ``out`` = (u (B x ld, unit column stride), status (B,), iters (B,)) preallocated device tensors."""
     if not problems:
         raise ValueError("no problems")

@@ -150,16 +150,15 @@ int carmpc_solve_batch_noalloc(const carmpc_problem* prob, int64_t batch, const 
                                const carmpc_settings* settings, hipStream_t stream);
 
 /* Several problems in one call: instances grouped by problem, segment j is
- * [offsets[j], offsets[j+1]) (host array of nprobs+1).  Row strides follow
- * each problem's n; u_out uses a common row stride ld_u >= max n.  The segments' launches are
- * forked onto internal side streams (event fork/join with `stream`), so one launch's tail
- * overlaps the next one's start; the call stays stream-ordered on `stream`. */
+ * [offsets[j], offsets[j+1]) (host array of nprobs+1).  Row strides follow each problem's n; u_out
+ * uses a common row stride ld_u >= max n.  Consecutive segments that run on the same instantiation
+ * of the grouped kernel (same horizon, same model structure; up to 4 per launch) are solved by ONE launch whose
+ * workgroups move from a drained segment to the remaining ones, so no segment ends with a launch
+ * tail of its own; other segments are launched one after another.  Stream-ordered on `stream`. */
 int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, const int64_t* offsets,
                           const double* x0, const double* xref, double* u_out, int64_t ld_u,
                           int32_t* status, int32_t* iters, const carmpc_settings* settings,
                           hipStream_t stream);
-/* 1 = launch the segments one after another on `stream` (no side streams), 0 = default fork. */
-void carmpc_set_serial_segments(int32_t serial);
 
 /* MPCOutputFBWithDisturbance (mpc.py:495-667): constant scalar disturbance d with
  * x+ = A x + B u + Bd d.  set_disturbance stores the row offsets Ed (x = T x0 + S u + ABd d,

@@ -1,6 +1,8 @@
-"""carmpc_solve_segments: several problems in one call, launches forked onto side streams and
-joined back.  Concurrent and serial launching give bitwise-identical results,
-equal to per-problem solves, and the call is ordered on the caller's stream."""
+"""carmpc_solve_segments: several problems in one call.  Segments that share a kernel
+instantiation are solved by one launch whose workgroups move between the problems; the results
+equal per-problem solves (every instance is solved by one 16-lane group with the same arithmetic
+whichever workgroup claims it), mixed horizons and kernels fall back to per-problem launches, and
+the call is ordered on the caller's stream."""
 import numpy as np
 import pytest
 
@@ -25,29 +27,52 @@ def _states(n, seed):
                             rng.uniform(0, 4, n)])
 
 
-def test_concurrent_equals_serial_equals_single(gpu_available):
+def test_one_launch_equals_per_problem_solves(gpu_available):
     import torch
-    from carmpc_amd import _native
-    from carmpc_amd.qp import solve_segments
+    from carmpc_amd.qp import SolverSettings, solve_segments
     probs = _problems()
-    counts = [3001, 1, 2500]
-    offsets = np.concatenate([[0], np.cumsum(counts)])
-    X = torch.as_tensor(_states(int(offsets[-1]), 1)).cuda()
-    lib = _native.load()
-    try:
-        lib.carmpc_set_serial_segments(0)
+    for counts in ([3001, 1, 2500], [40, 7000, 3], [5000, 0, 4000]):
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        X = torch.as_tensor(_states(int(offsets[-1]), 1)).cuda()
         u_c, s_c, i_c = solve_segments(probs, offsets, X)
-        lib.carmpc_set_serial_segments(1)
-        u_s, s_s, i_s = solve_segments(probs, offsets, X)
-    finally:
-        lib.carmpc_set_serial_segments(0)
+        u_k, s_k, i_k = solve_segments(probs, offsets, X, settings=SolverSettings(kernel=2))   # per-problem launches
+        torch.cuda.synchronize()
+        assert torch.equal(s_c, s_k)
+        for j, p in enumerate(probs):
+            sl = slice(int(offsets[j]), int(offsets[j + 1]))
+            u1, s1, i1 = p.solve(X[sl])
+            assert torch.equal(s1, s_c[sl]) and torch.equal(i1, i_c[sl])
+            ok = (s1 == 0)
+            assert torch.equal(u1[ok], u_c[sl, :p.n][ok])
+            assert float((u_k[sl, :p.n][ok] - u1[ok]).abs().max()) <= 1e-6 if bool(ok.any()) else True
+
+
+def test_mixed_horizons_and_many_segments(gpu_available):
+    """N = 10 and N = 20 problems in one call (different instantiations: separate launches) and more
+    segments than one launch carries."""
+    import torch
+    from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.mpc import MPCStateFB
+    from carmpc_amd.qp import solve_segments
+    p20 = _problems()
+    p10 = MPCStateFB(dt=DT_CONTROL, N=10, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT,
+                     env=ENVIRONMENTS["RoadEnv"](), terminal_set_dir=TERMINAL_SETS).qp
+    probs = [p20[0], p20[1], p10, p20[2], p20[0], p20[1], p20[2], p20[0]]
+    counts = [300, 200, 500, 100, 250, 1, 350, 299]
+    offsets = np.concatenate([[0], np.cumsum(counts)])
+    x = _states(int(offsets[-1]), 7)
+    x[offsets[2]:offsets[3], 0] = np.random.default_rng(2).uniform(22, 30, 500)     # feasible range at N = 10
+    X = torch.as_tensor(x).cuda()
+    u, st, it = solve_segments(probs, offsets, X)
     torch.cuda.synchronize()
-    assert torch.equal(u_c, u_s) and torch.equal(s_c, s_s) and torch.equal(i_c, i_s)
+    assert u.shape[1] == 40
     for j, p in enumerate(probs):
         sl = slice(int(offsets[j]), int(offsets[j + 1]))
-        u1, s1, _ = p.solve(X[sl])
-        assert torch.equal(s1, s_c[sl])
-        assert torch.equal(u1, u_c[sl, :p.n])
+        u1, s1, i1 = p.solve(X[sl])
+        assert torch.equal(s1, st[sl]) and torch.equal(i1, it[sl])
+        ok = s1 == 0
+        assert torch.equal(u1[ok], u[sl, :p.n][ok])
 
 
 def test_stream_ordering_on_side_stream(gpu_available):
