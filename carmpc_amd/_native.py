@@ -25,7 +25,7 @@ EXPORTS = ("carmpc_problem_create", "carmpc_problem_create_dense", "carmpc_probl
            "carmpc_problem_info", "carmpc_problem_get", "carmpc_solve_batch", "carmpc_solve_segments",
            "carmpc_observer_batch", "carmpc_plant_step_batch", "carmpc_canonical_flops_per_iter",
            "carmpc_last_error", "carmpc_version", "carmpc_problem_kernel",
-           "carmpc_executed_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
+           "carmpc_executed_flops_per_iter", "carmpc_issued_flops_per_iter", "carmpc_problem_set_disturbance", "carmpc_solve_batch_dist",
            "carmpc_observer_dist_batch", "carmpc_closed_loop_batch", "carmpc_lp_batch",
            "carmpc_hetero_create", "carmpc_hetero_destroy", "carmpc_hetero_linearize", "carmpc_hetero_solve",
            "carmpc_hetero_get", "carmpc_solve_batch_noalloc",
@@ -117,6 +117,7 @@ def load():
         "carmpc_version": ([], ctypes.c_char_p),
         "carmpc_problem_kernel": ([vp], ctypes.c_int),
         "carmpc_executed_flops_per_iter": ([vp, i32], ctypes.c_double),
+        "carmpc_issued_flops_per_iter": ([vp, i32], ctypes.c_double),
         "carmpc_problem_set_disturbance": ([vp, dp], ctypes.c_int),
         "carmpc_solve_batch_dist": ([vp, i64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(Settings), vp], ctypes.c_int),
         "carmpc_observer_dist_batch": ([vp, i64, vp, i32, dp, dp, dp, dp, dp, vp, vp, vp, i64, vp], ctypes.c_int),

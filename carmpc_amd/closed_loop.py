@@ -1,4 +1,4 @@
-"""Closed-loop runs of many cars at once, entirely on the GPU (SURVEY §8f row 1).
+"""Closed-loop runs of many cars at once, entirely on the GPU.
 
 ``run_closed_loop(controller, starts)`` is the runner loop of the reference examples
 for a batch of start states:
@@ -13,8 +13,7 @@ An infeasible QP ends an instance as ``OutsideTheRegionOfAttractionError`` would
 reference run.  Plant, observer, QP and the stop tests run as device kernels
 (``carmpc_closed_loop_batch``); the host only launches.
 
-``region_of_attraction(controller, grid)`` is the paper's grid search (SURVEY §8f row 1:
-many closed-loop simulations from a grid of start states) as one batched run.
+``region_of_attraction(controller, grid)`` is the paper's grid search (many closed-loop simulations from a grid of start states) as one batched run.
 """
 from __future__ import annotations
 

@@ -8,7 +8,7 @@
 //                                     a block of N rows on x_1..x_N
 //   step     lib/mpc.py:319,326,332   G = A_rows S, E = A_rows T, w0 = b_rows
 // Also writes Phi_m = A^m B (m = 0..N-1) and the 2-norm of every general row
-// (the host uses them to split x0-only rows and normalise, DESIGN.md §4).
+// (the host uses them to split x0-only rows and normalise).
 //
 // Sizes are tiny (N <= 32): one 256-thread workgroup, LDS for the powers of A.
 #include "carmpc_internal.h"

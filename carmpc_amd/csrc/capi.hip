@@ -399,7 +399,7 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
     return CARMPC_OK;
 }
 
-// Kernel choice for one launch (settings.kernel, DESIGN.md §4).
+// Kernel choice for one launch (settings.kernel).
 hipError_t launch_solve(const DevProblem& D, int64_t batch, const double* x0, const double* xref, double* u_out,
                         int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
@@ -526,12 +526,13 @@ int carmpc_problem_kernel(const carmpc_problem* P) {
 }
 
 // Flops one IPM iteration (predictor + corrector + one refinement) of the given kernel
-// actually performs (multiply-add = 2), DESIGN.md §5.  Masked/padded lanes not counted.
+// actually performs (multiply-add = 2).  Masked/padded lanes not counted.
 double carmpc_executed_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
     if (!P) return 0.0;
     const double n = P->dev.n, p = P->dev.p, N = P->dev.N;
     if (kernel == 7 || (kernel == 0 && P->dev.ric)) {
-        // grouped Riccati kernel, one copy of the (16-lane redundant) stage recursions:
+        // grouped Riccati kernel, every stage recursion counted once (the matrix-core passes pad it
+        // to full 4x4x4 products, see carmpc_issued_flops_per_iter):
         // per stage factorization + adjoint + 2 backward + 3 forward passes, per row the five
         // row phases (~212 flops), per input the box rows; bicycle sparsity when selected
         const bool bike = P->dev.ric == 2;
@@ -553,6 +554,18 @@ double carmpc_executed_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
     const double resid = pred + rows + 4.0 * n + rows + qy + 2.0 * adj;
     const double solve = rows + adj + trisolve + pred + rows;
     return mbuild + chol + resid + 3.0 * solve + (qy + 4.0 * n);
+}
+
+double carmpc_issued_flops_per_iter(const carmpc_problem* P, int32_t kernel) {
+    if (!P) return 0.0;
+    if ((kernel == 7 || (kernel == 0 && P->dev.ric))) {
+        // v_mfma_f64_4x4x4 per stage: factorization 14, adjoint 2, backward pass 5, forward pass 3
+        // (ipm_riccati.hip: factor_mm, adjoint_mm, back_mm, forward_mm), 128 flops per QP each;
+        // per iteration one factorization, one adjoint, two backward and three forward passes
+        const double n = P->dev.n, p = P->dev.p, N = P->dev.N;
+        return N * 128.0 * (14.0 + 2.0 + 2.0 * 5.0 + 3.0 * 3.0) + 212.0 * p + 60.0 * n;
+    }
+    return carmpc_executed_flops_per_iter(P, kernel);
 }
 
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p) {

@@ -13,7 +13,7 @@ constexpr double UNBOXED_BOUND = 1e9; // |u_i| assumed by the Farkas test for un
 constexpr double PRE_TOL = 1e-9;      // x0-only row tolerance
 constexpr double STEP_FRAC = 0.99;
 constexpr double ZERO_ROW = 1e-12;    // relative row-norm threshold for x0-only rows
-constexpr double REFINE_MU = 1e-6;    // corrector refinement only once mu <= REFINE_MU (DESIGN.md §3)
+constexpr double REFINE_MU = 1e-6;    // corrector refinement only once mu <= REFINE_MU
 
 // Small stage matrices by value (symmetrised Q, P, R): kernel arguments, so the grouped
 // kernel reads them through the scalar cache.

@@ -1,4 +1,4 @@
-// Per-instance linearisation and condensed-QP assembly on the device (SURVEY §8f row 2).
+// Per-instance linearisation and condensed-QP assembly on the device.
 //
 // Every instance b carries its own linearisation point (x_e, u_e); the reference computes one
 // per controller in MPC.__init__:

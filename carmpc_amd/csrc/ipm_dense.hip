@@ -1,13 +1,13 @@
 // ipm_dense.hip -- dense condensed-QP Mehrotra IPM, one wavefront per QP (gfx950).
 //
 // Replaces the per-step cvxpy solve of lib/mpc.py:334-335 (MPCStateFB.step) and
-// lib/mpc.py:477-478 (MPCOutputFB.step).  Algorithm: DESIGN.md §3, restated on the
+// lib/mpc.py:477-478 (MPCOutputFB.step).  Algorithm: Mehrotra predictor-corrector IPM, restated on the
 // CPU in oracle/qp.py::ipm and oracle/ipm.c (same steps, same tolerances):
 //   Mehrotra predictor-corrector on the normal equations M = H + G'diag(z/s)G + box,
 //   one iterative-refinement pass on the corrector, box-Farkas infeasibility
 //   certificate, and an active-set polish once mu <= POLISH_MU.
 //
-// Layout (DESIGN.md §4):
+// Layout:
 //   * one workgroup = WPB wavefronts sharing one problem (environment); G (p x ldg,
 //     unit rows, ldg = NV+2 doubles, 16B-aligned rows) and H (NV x NV) live in LDS;
 //   * lane i < NV owns decision variable i: u_i, its box slacks/duals, and column i

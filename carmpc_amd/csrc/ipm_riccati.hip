@@ -1,7 +1,7 @@
 // ipm_riccati.hip -- grouped stage-form Mehrotra IPM: 16 lanes per QP, 4 QPs per wavefront.
 //
-// Replaces the per-step cvxpy solve of lib/mpc.py:334-335 / 477-478 with the algorithm of
-// DESIGN.md §3 (oracle/qp.py::ipm), applying M^{-1} by a backward Riccati recursion and a
+// Replaces the per-step cvxpy solve of lib/mpc.py:334-335 / 477-478 with a Mehrotra
+// predictor-corrector IPM (restated on the CPU in oracle/qp.py::ipm), applying M^{-1} by a backward Riccati recursion and a
 // forward roll-out over the horizon (oracle/riccati.py, the CPU restatement this kernel
 // follows line by line).  Every QP row acts on one predicted state x_k (mpc.py:196-253),
 // and H = R_hat + S'Q_hat S (matrix_gen.py:35-72), so
@@ -1238,7 +1238,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
             // ================= solves =================
             // fully unrolled: k is a constant in every branch below (precise register lifetimes)
             // the refinement solve (k = 2 of a normal trip) only once mu <= REFINE_MU; before
-            // that its correction is zero (DESIGN.md §3)
+            // that its correction is zero
             const bool refine = mu <= REFINE_MU;
 #pragma unroll
             for (int k = 0; k < POLISH_REFINE + 1; ++k) {
@@ -1413,7 +1413,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                 // predictor and rc = s z + dsA dzA - smu for the corrector (dsA, dzA from dyA).
                 if (k == 0) {
                     double amax = INFINITY, mua = -0.0;
-                    double kd[2][2][4], dsv[RS], dzv[RS];
+                    double dsv[RS], dzv[RS];
 #pragma unroll
                     for (int s = 0; s < RS; ++s) {
                         const int sg = s / RSEG;
@@ -1438,10 +1438,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                                 const double dzu = (-su * zu - zu * dsu) * frcp(su);
                                 const double dzl = (-sl * zl - zl * dsl) * frcp(sl);
                                 amax = fmin(amax, fmin(fmin(ratio(su, dsu), ratio(zu, dzu)), fmin(ratio(sl, dsl), ratio(zl, dzl))));
-                                kd[sg][c][0] = dsu;
-                                kd[sg][c][1] = dzu;
-                                kd[sg][c][2] = dsl;
-                                kd[sg][c][3] = dzl;
+                                // parked in the input's state row (fields that are free until k = 1) across the reduction
+                                BX(F_E1, sg, c) = dsu;
+                                BX(F_E2, sg, c) = dzu;
+                                BX(F_E3, sg, c) = dsl;
+                                BX(F_E4, sg, c) = dzl;
                             }
                         }
                     const double a = fmin(1.0, row_min(amax));
@@ -1452,10 +1453,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                         for (int c = 0; c < 2; ++c)
                             if (own[sg] && boxed) {
-                                mua = fma(fma(a, kd[sg][c][0], BX(F_SU, sg, c)), fma(a, kd[sg][c][1], BX(F_ZU, sg, c)), mua);
-                                mua = fma(fma(a, kd[sg][c][2], BX(F_SL, sg, c)), fma(a, kd[sg][c][3], BX(F_ZL, sg, c)), mua);
-                                BX(F_E1, sg, c) = kd[sg][c][0] * kd[sg][c][1];   // predictor products, kept for k = 1
-                                BX(F_E2, sg, c) = kd[sg][c][2] * kd[sg][c][3];
+                                const double dsu = BX(F_E1, sg, c), dzu = BX(F_E2, sg, c);
+                                const double dsl = BX(F_E3, sg, c), dzl = BX(F_E4, sg, c);
+                                mua = fma(fma(a, dsu, BX(F_SU, sg, c)), fma(a, dzu, BX(F_ZU, sg, c)), mua);
+                                mua = fma(fma(a, dsl, BX(F_SL, sg, c)), fma(a, dzl, BX(F_ZL, sg, c)), mua);
+                                BX(F_E1, sg, c) = dsu * dzu;   // predictor products, kept for k = 1
+                                BX(F_E2, sg, c) = dsl * dzl;
                             }
                     const double sg3 = row_sum(mua) * inv_m / mu;
                     smu = sg3 * sg3 * sg3 * mu;

@@ -1,6 +1,6 @@
 // ipm_staged.hip -- stage-structured condensed-QP Mehrotra IPM, one wavefront per QP (gfx950).
 //
-// Same algorithm, tolerances and trip structure as ipm_dense.hip (DESIGN.md §3; CPU
+// Same algorithm, tolerances and trip structure as ipm_dense.hip (CPU
 // restatement oracle/qp.py::ipm, oracle/ipm.c), replacing the per-step cvxpy solve of
 // lib/mpc.py:334-335 / 477-478.  What changes is how the products with G, H and the
 // normal matrix are formed: every QP row of the reference acts on ONE predicted state
@@ -987,8 +987,10 @@ template <int N>
 hipError_t launch_rs(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
                      int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
     // default (2): LDS-broadcast Cholesky with square roots, 8 waves per workgroup (fastest
-    // measured); A/B variants: 4 readlane-broadcast Cholesky, 5 four waves per
-    // workgroup (one wave per SIMD, 512 registers), 6 square-root-free LDL'.
+    // measured).  The variants it was measured against -- 4 readlane-broadcast Cholesky, 5 four
+    // waves per workgroup (one wave per SIMD, 512 registers), 6 square-root-free LDL' -- are
+    // only instantiated in experiment builds (-DCARMPC_AB_KERNELS); the product library rejects
+    // settings.kernel 4..6 (launch_staged).
 #define CARMPC_RS_SWITCH(LDS, WPB)                                                                    \
     switch (P.srs) {                                                                                  \
         case 1: return launch_t<N, 1, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
@@ -997,9 +999,11 @@ hipError_t launch_rs(const DevProblem& P, int64_t batch, const double* x0, const
         case 4: return launch_t<N, 4, LDS, WPB>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream); \
         default: return hipErrorInvalidValue;                                                         \
     }
+#ifdef CARMPC_AB_KERNELS
     if (s.kernel == 4) { CARMPC_RS_SWITCH(0, 8) }
     if (s.kernel == 5) { CARMPC_RS_SWITCH(1, 4) }
     if (s.kernel == 6) { CARMPC_RS_SWITCH(2, 8) }
+#endif
     CARMPC_RS_SWITCH(1, 8)
 #undef CARMPC_RS_SWITCH
 }
@@ -1020,6 +1024,12 @@ hipError_t launch_staged(const DevProblem& P, int64_t batch, const double* x0, c
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
+#ifndef CARMPC_AB_KERNELS
+    if (s.kernel >= 4 && s.kernel <= 6) {
+        *unsupported = 1;
+        return hipErrorInvalidValue;
+    }
+#endif
     switch (P.N) {
         case 10: return launch_rs<10>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);
         case 20: return launch_rs<20>(P, batch, x0, xref, u_out, ld_u, status, iters, s, stream);

@@ -1,4 +1,4 @@
-// Batched small LPs for the terminal-set synthesis (SURVEY §8f row 3):
+// Batched small LPs for the terminal-set synthesis:
 //   maximise c'x  s.t.  A x <= b,  x in R^4,
 // one LP per wavefront.  lib/terminal_set.py:45-67 solves one cvxpy LP per state row and
 // horizon; polytope.reduce solves one per candidate half-space.  Here every LP of one

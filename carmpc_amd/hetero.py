@@ -1,5 +1,4 @@
-"""Many MPCStateFB controllers, each linearised at its own point, solved in one batch
-(SURVEY §8f row 2).
+"""Many MPCStateFB controllers, each linearised at its own point, solved in one batch.
 
 The reference builds one controller per linearisation point: ``MPC.__init__`` linearises
 (mpc.py:128-161), discretises (mpc.py:164-180), solves the DARE (mpc.py:67-74), forms K

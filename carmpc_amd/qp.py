@@ -51,7 +51,7 @@ def require_gpu(device=None) -> torch.device:
 
 @dataclass
 class SolverSettings:
-    """carmpc_settings; defaults match oracle/qp.py (DESIGN.md §3)."""
+    """carmpc_settings; defaults match oracle/qp.py."""
     tol: float = 1e-10
     tol_mu: float = 1e-12
     max_iter: int = 60
@@ -120,7 +120,7 @@ class QPProblem:
         vals = [ctypes.c_int32() for _ in range(5)]
         check(_native.load().carmpc_problem_info(self._h, *[ctypes.byref(v) for v in vals]), "carmpc_problem_info")
         self.n, self.p, self.npre, self.nx, _ = (v.value for v in vals)
-        #: solve kernel chosen by ``kernel=0`` (auto): 1 dense, 2 staged, 7 grouped Riccati (DESIGN.md §4)
+        #: solve kernel chosen by ``kernel=0`` (auto): 1 dense, 2 staged, 7 grouped Riccati
         self.kernel = int(_native.load().carmpc_problem_kernel(self._h))
 
     def __del__(self):
@@ -150,12 +150,16 @@ class QPProblem:
         return out
 
     def canonical_flops_per_iter(self) -> float:
-        """p n^2 + n^3/3 + 6 n^2 + 12 p n with p = general (QP) rows."""
+        """Canonical dense-IPM count: p n^2 + n^3/3 + 6 n^2 + 12 p n with p = general (QP) rows."""
         return float(_native.load().carmpc_canonical_flops_per_iter(self.n, self.p))
 
     def executed_flops_per_iter(self, kernel: int = 0) -> float:
-        """Flops per IPM iteration the chosen kernel actually executes."""
+        """Flops per IPM iteration the chosen kernel performs for one QP (every recursion counted once)."""
         return float(_native.load().carmpc_executed_flops_per_iter(self._h, kernel))
+
+    def issued_flops_per_iter(self, kernel: int = 0) -> float:
+        """The same with every matrix-core instruction counted as a full 4x4x4 product."""
+        return float(_native.load().carmpc_issued_flops_per_iter(self._h, kernel))
 
     # ----------------------------------------------------------------- solve
     def set_disturbance(self, Bd) -> None:

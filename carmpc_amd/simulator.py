@@ -3,7 +3,7 @@
 ``CarSimulator`` is the reference's scalar plant (the *caller* of the QP path,
 kept so the example loops run unchanged).  ``BatchCarSimulator`` steps B
 plants at once on the GPU with the ``carmpc_plant_step_batch`` kernel
-(SURVEY §8f-1), so a whole closed loop stays on the device.
+so a whole closed loop stays on the device.
 """
 from __future__ import annotations
 

@@ -1,4 +1,4 @@
-"""Terminal-set synthesis with the LPs on the GPU (mirrors lib/terminal_set.py; SURVEY §8f row 3).
+"""Terminal-set synthesis with the LPs on the GPU (mirrors lib/terminal_set.py).
 
 Same functions and file format as the reference:
 

@@ -81,7 +81,7 @@ typedef struct {
     const double* goal;   /* nx  default reference (mpc.py:46,182-194)                 */
 } carmpc_model_desc;
 
-/* Solver settings (DESIGN.md §3).  Pass NULL for the defaults
+/* Solver settings.  Pass NULL for the defaults
  * {1e-10, 1e-12, 60}. */
 typedef struct {
     double tol;        /* primal/dual residual tolerance, relative to 1+||.||_inf */
@@ -90,7 +90,8 @@ typedef struct {
     int32_t kernel;    /* 0 = auto (grouped Riccati, else staged, else dense), 1 = dense
                           (G,H in LDS), 2 = staged (stage structure, assembled problems
                           with nu=2 and a compiled N), 3 = dense with 4 waves per
-                          workgroup, 4-6 staged A/B variants, 7 = grouped stage-form
+                          workgroup, 4-6 = staged variants of experiment builds only (rejected
+                          with CARMPC_EUNSUPPORTED otherwise), 7 = grouped stage-form
                           (Riccati) kernel, 16 lanes per QP (assembled, nu=2, N in
                           {10,20}, <= 8 rows per stage) */
 } carmpc_settings;
@@ -98,9 +99,15 @@ typedef struct {
 /* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged, 7 grouped Riccati. */
 int carmpc_problem_kernel(const carmpc_problem* prob);
 
-/* Flops per IPM iteration the given kernel (0 auto, 1 dense, 2 staged, 7 Riccati) executes; the
- * canonical dense count of SURVEY §8d is carmpc_canonical_flops_per_iter. */
+/* Flops per IPM iteration the given kernel (0 auto, 1 dense, 2 staged, 7 Riccati) performs on
+ * behalf of one QP, counting every stage recursion once (useful work); the canonical dense-IPM
+ * count is carmpc_canonical_flops_per_iter. */
 double carmpc_executed_flops_per_iter(const carmpc_problem* prob, int32_t kernel);
+/* Flops per IPM iteration the hardware is asked to perform for one QP: as above, except that
+ * every matrix-core instruction of the Riccati kernel counts as a full 4x4x4 product (128 flops
+ * per QP) although part of its operands are structural zeros or replicated columns.  Equals
+ * carmpc_executed_flops_per_iter for kernels that issue no matrix-core instructions. */
+double carmpc_issued_flops_per_iter(const carmpc_problem* prob, int32_t kernel);
 
 /* Build one problem on the current device (assembly kernel + row normalisation). */
 int carmpc_problem_create(const carmpc_model_desc* desc, carmpc_problem** out);
@@ -201,7 +208,7 @@ int carmpc_observer_batch(const carmpc_problem* prob, int64_t batch, const doubl
 int carmpc_plant_step_batch(int64_t batch, double* state, const double* u, int64_t ld_u, double dt,
                             double l1, int32_t* bad, hipStream_t stream);
 
-/* ---- closed loop on the device (SURVEY §8f row 1) -------------------------------------
+/* ---- closed loop on the device -------------------------------------
  * The examples' runner loops for B independent cars, entirely on the GPU:
  *   examples/run_MPCStateFB.py:26-43   mode 0: u = controller.step(state)
  *   examples/run_MPCOutputFB.py:28-50  mode 1: u = controller.step(C state) (Luenberger, mpc.py:439-492)
@@ -244,7 +251,7 @@ int carmpc_closed_loop_batch(const carmpc_problem* prob, int64_t batch, const ca
                              int32_t* outcome, int32_t* steps, int32_t check_every,
                              const carmpc_settings* settings, hipStream_t stream);
 
-/* ---- batched small LPs (terminal-set synthesis, SURVEY §8f row 3) ------------------------
+/* ---- batched small LPs (terminal-set synthesis) ------------------------
  * lib/terminal_set.py:45-67 (one LP per state row and horizon k) and the redundancy removal of
  * the final set (polytope.reduce, called at terminal_set.py:197) as one launch:
  *   LP l:  maximise c_l'x  s.t.  A_l x <= b_l (+ relax_amount on row relax[l]),  x in R^4
@@ -262,7 +269,7 @@ int carmpc_lp_batch(int64_t nlp, int32_t max_m, const int64_t* a_off, const int6
                     double relax_amount, double* value, double* x, int32_t* status, int32_t* iters,
                     hipStream_t stream);
 
-/* ---- per-instance linearisation (SURVEY §8f row 2) -------------------------------------
+/* ---- per-instance linearisation -------------------------------------
  * Every instance b has its own linearisation point (lin_state[b], lin_input[b]): A, B
  * (mpc.py:128-180), P = DARE (mpc.py:67-74; zeros when no stabilising solution), K (mpc.py:80-81)
  * and the condensed QP (matrix_gen.py:6-72, mpc.py:196-253) are built on the device, one slice per
@@ -323,7 +330,7 @@ int carmpc_cpu_solve_batch_dist(const carmpc_cpu_problem* prob, int64_t batch, c
                                 const carmpc_settings* settings, int32_t threads);
 
 /* Canonical per-iteration flop count of the dense condensed IPM
- * (SURVEY §8d): p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
+ * p*n^2 + n^3/3 + 6n^2 + 12pn with p = general rows. */
 double carmpc_canonical_flops_per_iter(int32_t n, int32_t p);
 
 const char* carmpc_last_error(void);

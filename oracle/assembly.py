@@ -5,7 +5,7 @@ the product package; ``carmpc_amd`` performs the same assembly with its own
 HIP kernel (``carmpc_amd/csrc/carmpc_assembly.hip``) and the tests compare the
 two.
 
-Notation (shared with DESIGN.md): nx=4, nu=2, n=N*nu decision variables
+Notation: nx=4, nu=2, n=N*nu decision variables
 ``ubar=(u_0..u_{N-1})``; the reference QP at state x0 is
 
     min_u  1/2 u'Hu + (h (x0-goal))'u

@@ -9,7 +9,7 @@
  *     min 1/2 u'Hu + q'u,  q = hq (x0 - xref)          (mpc.py:320-321)
  *     s.t. G u <= w0 - E x0  (terminal + state rows)    (mpc.py:319,324-332)
  *          lb <= u <= ub     (input box)                (mpc.py:327-329)
- * with the algorithm of DESIGN.md §3 / oracle/qp.py::ipm: dense Mehrotra
+ * with the algorithm of oracle/qp.py::ipm: dense Mehrotra
  * predictor-corrector on the normal equations, one refinement pass on the
  * corrector, rigorous box-Farkas infeasibility test, and the active-set polish.
  * OpenMP over instances.  G/w0/E rows are the normalised QP rows; pre_* are

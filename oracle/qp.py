@@ -7,8 +7,8 @@ unpinned upstream, so the QP arithmetic cannot be run from the reference; see
 ``oracle/__init__.py`` for how parity is anchored instead.
 
 This module provides
-  * ``ipm``        -- the dense Mehrotra predictor-corrector IPM specified in
-                      DESIGN.md §3 (the algorithm the HIP kernel implements),
+  * ``ipm``        -- the dense Mehrotra predictor-corrector IPM (the algorithm
+                      the HIP kernels implement),
                       vectorised numpy, one instance at a time;
   * ``certify``    -- an independent active-set KKT polish + certificate: returns
                       the exact optimum (to ~1e-13) and the KKT residuals, so a
@@ -26,7 +26,7 @@ from scipy.optimize import linprog
 STATUS_OPTIMAL, STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL = 0, 1, 2, 3
 STATUS_NAMES = {0: "optimal", 1: "primal_infeasible", 2: "max_iter", 3: "numerical"}
 
-# Settings shared with oracle/ipm.c and carmpc_amd/csrc (DESIGN.md §3)
+# Settings shared with oracle/ipm.c and carmpc_amd/csrc
 TOL_RES = 1e-10
 TOL_MU = 1e-12
 MAX_ITER = 60
@@ -58,7 +58,7 @@ def opposite_pairs(G, w0, E):
 
     Such a pair writes an equality c'x = b as two inequalities -- the reference's
     fallback terminal set x_N = goal (lib/mpc.py:107-117) does exactly that.  When both
-    rows are active the polish may re-split their multipliers (DESIGN.md §3.4)."""
+    rows are active the polish may re-split their multipliers."""
     p = G.shape[0]
     partner = np.full(p, -1, dtype=np.int32)
     if p == 0:
@@ -197,7 +197,7 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
 
 def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE,
                 partner=None):
-    """Active-set polish (DESIGN.md §3.4).  Active set from the IPM iterate (s < z); solve the
+    """Active-set polish.  Active set from the IPM iterate (s < z); solve the
     equality-constrained KKT [[H, A'], [A, 0]] [x; y] = [-q; b_act] by iterative refinement on
     the regularised factor  H + A'A/delta  (the IPM's M with d = 1/delta on active rows, 0 else);
     accept only if x is primal feasible and the active multipliers are nonnegative.  Rows whose

@@ -1,6 +1,6 @@
 """Stage-form (Riccati) restatement of the per-step QP IPM (ORACLE, tests only).
 
-Same algorithm, tolerances and trip structure as ``oracle/qp.py::ipm`` (DESIGN.md §3):
+Same algorithm, tolerances and trip structure as ``oracle/qp.py::ipm``:
 the Newton system  M du = b,  M = H + G'DG + diag(box),  is the KKT system of a
 linear-quadratic problem over the horizon, because every QP row of the reference acts
 on ONE predicted state (``lib/mpc.py:196-253``: terminal rows on x_N, state rows on

@@ -31,7 +31,7 @@ def test_host_only_entry_points():
     from carmpc_amd import _native
     lib = _native.load()
     assert _native.version().startswith("carmpc-mi355x")
-    # SURVEY §8d canonical count: p n^2 + n^3/3 + 6 n^2 + 12 p n
+    # canonical dense-IPM count: p n^2 + n^3/3 + 6 n^2 + 12 p n
     assert abs(lib.carmpc_canonical_flops_per_iter(40, 202) - 451093.333) < 1e-2
     assert abs(lib.carmpc_canonical_flops_per_iter(20, 85) - 59466.667) < 1e-2
     # argument validation happens before any device call

@@ -21,7 +21,7 @@ def test_runner_stop_indices():
 
 def test_example_runs():
     """The examples' own start states: StateFB reaches the goal box after 52 loop indices,
-    OutputFB runs to its 76-index time-out (SURVEY §3)."""
+    OutputFB runs to its 76-index time-out."""
     from oracle import closed_loop as ocl
     asm = _asm()
     solve = ocl.c_solver(asm)

@@ -39,7 +39,7 @@ def test_statefb_closed_loop_matches_golden(gpu_available):
 
 
 def test_statefb_infeasible_start_raises(gpu_available):
-    """the example's start state is infeasible at N=10."""
+    """Configuration 1 (run_MPCStateFB, RoadEnv, N=10): the example's start state is infeasible at N=10."""
     from carmpc_amd.environments import RoadEnv
     from carmpc_amd.mpc import MPCStateFB, OutsideTheRegionOfAttractionError
     c = MPCStateFB(0.2, 10, [0, 0, 0, 3], [0, 0], env=RoadEnv(), terminal_set_dir=TERMINAL_SETS)

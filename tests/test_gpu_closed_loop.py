@@ -1,4 +1,4 @@
-"""GPU parity of the device closed loop (carmpc_closed_loop_batch, SURVEY §8f row 1) against
+"""GPU parity of the device closed loop (carmpc_closed_loop_batch) against
 the CPU restatement of the examples' runner loops (oracle/closed_loop.py).
 
 Per instance: identical outcome (reached / infeasible / time-out ...) and step count, final

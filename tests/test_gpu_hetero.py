@@ -1,4 +1,4 @@
-"""GPU parity of per-instance linearisation (carmpc_hetero_*, SURVEY §8f row 2).
+"""GPU parity of per-instance linearisation (carmpc_hetero_*).
 
 Against oracle/assembly.py::build at each instance's linearisation point (which restates
 mpc.py:22-117 and matrix_gen.py:6-72, with scipy's DARE as the reference calls it):

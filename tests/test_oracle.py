@@ -120,7 +120,7 @@ def test_environment_and_configuration_data():
 
 
 def test_terminal_set_files_are_reference_copies():
-    # byte-identical copies of the reference data (md5 recorded in DESIGN.md)
+    # byte-identical copies of the reference data
     import hashlib
     want = {"RoadEnv_30_1.5_0_0.npy": "b8e85fd87a9d03968feeb45884bce20f",
             "RoadMultipleCarsEnv_30_1.5_0_0.npy": "e51cd11d0a547780b53b624cc09eeacf",

@@ -1,7 +1,7 @@
 """The stage-form (Riccati) restatement of the IPM follows the dense oracle step for step.
 
 oracle/riccati.py is the arithmetic of the grouped HIP kernel (ipm_riccati.hip): same
-algorithm as oracle/qp.py::ipm (DESIGN.md §3), with M^{-1} applied by a backward Riccati
+algorithm as oracle/qp.py::ipm, with M^{-1} applied by a backward Riccati
 recursion + forward roll-out over the horizon instead of a dense Cholesky.
 """
 import numpy as np

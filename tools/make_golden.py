@@ -51,7 +51,7 @@ CONFIGS = [("RoadEnv", 10), ("RoadEnv", 20), ("RoadOneCarEnv", 20), ("RoadMultip
 
 
 def sample_x0(rng, goal_x, k):
-    """Survey §8d input distribution: x in [g_x-25, g_x], y in [-3,3], psi in [-pi/8,pi/8], v in [-1,5]."""
+    """Input distribution of the benchmark configurations: x in [g_x-25, g_x], y in [-3,3], psi in [-pi/8,pi/8], v in [-1,5]."""
     return np.stack([rng.uniform(goal_x - 25, goal_x, k), rng.uniform(-3, 3, k),
                      rng.uniform(-np.pi / 8, np.pi / 8, k), rng.uniform(-1, 5, k)], axis=1)
 
