@@ -23,7 +23,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
 # Per-file code generation: the Riccati kernel runs one wave per SIMD and is latency-bound in
 # its stage recursions; the iterative ILP scheduler gains ~3 % there (tools/gpu/sched_sweep.sh:
 # 6.71M -> 6.91M QP/s; max-ilp, max-memory-clause, iterative-minreg/maxocc were slower).
-FILE_FLAGS = {"ipm_riccati.hip": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]}
+# --amdgpu-mfma-vgpr-form keeps the matrix-core results in ordinary registers: they feed vector
+# FMAs at once, and the default (accumulation-register results) cost ~19 register moves per stage
+# of the factorization pass (10.07M -> 10.35M QP/s).
+FILE_FLAGS = {"ipm_riccati.hip": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp", "-mllvm", "--amdgpu-mfma-vgpr-form"]}
 
 
 def _hipcc():

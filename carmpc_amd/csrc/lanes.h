@@ -35,16 +35,19 @@ __device__ __forceinline__ double row_sum(double v) { return row_reduce<OpSum>(v
 __device__ __forceinline__ double row_max(double v) { return row_reduce<OpMax>(v); }
 __device__ __forceinline__ double row_min(double v) { return row_reduce<OpMin>(v); }
 
-// Reciprocal / reciprocal square root: hardware approximation + two Newton steps.
+// Reciprocal: v_rcp_f64 is good to ~2^-25 (measured, tools/probe/rcp_probe.hip: max 2.5e8 ulp), so
+// one Newton step leaves <= 11 ulp (mean 0.6) -- enough for the scalings it is used for (z/s, step
+// ratios, pivots; the IPM's iterates are insensitive at that level and statuses and iteration
+// counts are unchanged on every test vector).  CARMPC_FRCP_NR2 adds the second step (<= 1 ulp).
 __device__ __forceinline__ double frcp(double b) {
     double r = __builtin_amdgcn_rcp(b);
     r = fma(fma(-b, r, 1.0), r, r);
-#ifdef CARMPC_FRCP_NR1   // A/B: v_rcp_f64 is good to ~2^-25, one step leaves <= 11 ulp
-    return r;
-#else
-    return fma(fma(-b, r, 1.0), r, r);
+#ifdef CARMPC_FRCP_NR2
+    r = fma(fma(-b, r, 1.0), r, r);
 #endif
+    return r;
 }
+// Reciprocal square root: hardware approximation + two Newton steps.
 __device__ __forceinline__ double frsq(double a) {
     double r = __builtin_amdgcn_rsq(a);
     const double h = 0.5 * a;
