@@ -323,18 +323,31 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
         HIP_TRY(hipMemcpy(w0p.data(), D.w0, sizeof(double) * w0p.size(), hipMemcpyDeviceToHost), "readback w0");
         HIP_TRY(hipMemcpy(Ep.data(), D.E, sizeof(double) * Ep.size(), hipMemcpyDeviceToHost), "readback E");
     }
+    // slots per segment: the smallest count that holds every stage k < N in its owner's segment and
+    // the stage-N rows in the owner of N plus the overflow segments (kernels skip the slots above it)
+    int per_stage[33] = {};
+    for (int r = 0; r < D.p; ++r) {
+        const int k = stage[r];
+        if (k < 1 || k > N) return CARMPC_OK;
+        ++per_stage[k];
+    }
+    int rseg = 1, n_over = 0;
+    for (int k = 1; k < N; ++k) rseg = std::max(rseg, per_stage[k]);
+    for (int s2 = 0; s2 < 2; ++s2)
+        for (int j2 = 0; j2 < 16; ++j2) n_over += (j2 + 1 + 16 * s2 > N) ? 1 : 0;
+    rseg = std::max(rseg, (per_stage[N] + n_over) / (n_over + 1));   // ceil(rows_N / (owner + overflow segments))
+    if (rseg > kRicSeg) return CARMPC_OK;
     int cnt[2][16] = {};
     std::vector<int32_t> slot_of(D.p, -1);
     for (int r = 0; r < D.p; ++r) {
         const int k = stage[r];
-        if (k < 1 || k > N) return CARMPC_OK;
         int sg = (k - 1) / 16, j = (k - 1) % 16;
-        if (cnt[sg][j] >= kRicSeg) {
+        if (cnt[sg][j] >= rseg) {
             if (k != N) return CARMPC_OK;
             int best = -1;
             for (int s2 = 0; s2 < 2; ++s2)
                 for (int j2 = 0; j2 < 16; ++j2)
-                    if (j2 + 1 + 16 * s2 > N && cnt[s2][j2] < kRicSeg && (best < 0 || cnt[s2][j2] < cnt[best / 16][best % 16]))
+                    if (j2 + 1 + 16 * s2 > N && cnt[s2][j2] < rseg && (best < 0 || cnt[s2][j2] < cnt[best / 16][best % 16]))
                         best = s2 * 16 + j2;
             if (best < 0) return CARMPC_OK;
             sg = best / 16;
@@ -394,6 +407,7 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
                       M.A[15] == 1.0 && zero_outside(M.B, 4, 2, keepB, 2) && zero_outside(M.Q, 4, 4, keepQ, 4) &&
                       zero_outside(M.R, 2, 2, keepR, 2);
     D.ric = bike ? 2 : 1;
+    D.rseg = rseg;
     P->ric_slot = slot_of;
     *ok = true;
     return CARMPC_OK;
@@ -805,25 +819,20 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
     if (live.empty()) return CARMPC_OK;
     if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
     // Runs of consecutive segments that share one instantiation of the grouped Riccati kernel go out
-    // as ONE launch (ipm_riccati_segs_kernel: workgroups move from a drained segment to the others),
+    // as ONE launch sequence (ipm_riccati.hip: workgroups move from a drained segment to the others),
     // so no segment ends with its own launch tail; anything else is launched per problem.  All
-    // launches are queued on `stream`, one claim counter per segment from one stream-ordered block.
+    // launches are queued on `stream`; counters and work lists are stream-ordered allocations of
+    // the launch helpers.
     auto ric_ok = [&](int j) { return (s.kernel == 0 || s.kernel == 7) && probs[j]->dev.ric != 0; };
-    unsigned* counters = nullptr;
-    const size_t ncount = (size_t)kRicClaimStride * live.size();
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&counters), sizeof(unsigned) * ncount, stream), "segment counters");
     int rc = CARMPC_OK;
-    hipError_t e = launch_zero_u32(counters, (int)ncount, stream);
-    if (e != hipSuccess) rc = hipfail(e, "zero segment counters");
     for (size_t i = 0; i < live.size() && rc == CARMPC_OK;) {
         size_t i1 = i + 1;
         if (ric_ok(live[i]))
             while (i1 < live.size() && i1 - i < (size_t)kRicMaxSeg && live[i1] == live[i1 - 1] + 1 && ric_ok(live[i1]) &&
                    probs[live[i1]]->dev.N == probs[live[i]]->dev.N && probs[live[i1]]->dev.ric == probs[live[i]]->dev.ric)
                 ++i1;
-        Settings sk = s;
-        sk.claim = counters + kRicClaimStride * i;
         int unsupported = 0;
+        hipError_t e = hipSuccess;
         if (i1 - i >= 2) {
             RicSegs T{};
             T.nseg = (int)(i1 - i);
@@ -832,19 +841,17 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
                 T.P[k - i] = probs[live[k]]->dev;
             }
             T.off[i1 - i] = offsets[live[i1 - 1] + 1];
-            e = launch_riccati_segs(T, x0, xref, u_out, ld_u, status, iters, sk, stream, &unsupported);
+            e = launch_riccati_segs(T, x0, xref, u_out, ld_u, status, iters, s, stream, &unsupported);
         } else {
             const int j = live[i];
             const int64_t b0 = offsets[j], b1 = offsets[j + 1];
             e = launch_solve(probs[j]->dev, b1 - b0, x0 + b0 * NX, xref ? xref + b0 * NX : nullptr, u_out + b0 * ld_u, ld_u,
-                             status + b0, iters ? iters + b0 : nullptr, sk, stream, &unsupported);
+                             status + b0, iters ? iters + b0 : nullptr, s, stream, &unsupported);
         }
         if (unsupported) rc = fail(CARMPC_EUNSUPPORTED, "no compiled kernel for this problem size");
         else if (e != hipSuccess) rc = hipfail(e, "segment launch");
         i = i1;
     }
-    e = hipFreeAsync(counters, stream);
-    if (rc == CARMPC_OK && e != hipSuccess) rc = hipfail(e, "free segment counters");
     return rc;
 }
 

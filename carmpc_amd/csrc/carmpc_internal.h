@@ -67,7 +67,8 @@ struct DevProblem {
     const int32_t* s_partner; // srs*64: slot index of the opposite row or -1 (staged kernel)
     // grouped Riccati layout (ipm_riccati.hip, capi.hip::riccati_layout): 16 lanes per QP,
     // lane j owns stage j+1 (segment 0) and j+17 (segment 1); slot e = (seg*8 + s)*16 + j
-    int32_t ric;              // layout present
+    int32_t ric;              // layout present: 1 dense stage matrices, 2 bicycle sparsity
+    int32_t rseg;             // slots per segment in use (every lane): the kernels skip the rest
     const double* r_coef;     // 256 x NX  normalised row coefficients c~ of each slot
     const double* r_w0;       // 256
     const double* r_E;        // 256 x NX
@@ -278,6 +279,18 @@ struct RicSegs {
     int32_t nseg;
     int64_t off[kRicMaxSeg + 1];
     DevProblem P[kRicMaxSeg];
+};
+// Work lists of the Riccati launch pipeline (ipm_riccati.hip: iterations -> polish -> retry), device
+// memory for one call.  cnt holds kRicClaimStride words per segment: [0] claim counter of the iteration
+// launch, [1] number of handed-off instances, [2] claim counter of the polish launch, [3] number of
+// rejected polishes, [4] claim counter of the retry launch.  The index lists are per segment, starting at
+// the segment's first instance; masks and iteration counts are stored per instance.  All null: no pipeline.
+struct RicWork {
+    unsigned* cnt;
+    int32_t* pend_idx;    // total: segment-relative rows awaiting the polish
+    int32_t* pend_it;     // total: IPM iterations done at the hand-off
+    int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
+    uint32_t* pend_mask;  // total x 16 lanes: bit s = row slot s active, bits 16.. = box rows of the owned inputs
 };
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                                int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported);

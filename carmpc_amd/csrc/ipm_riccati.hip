@@ -203,12 +203,26 @@ struct MtH {
 // segment until that counter runs out, then moves on round-robin to help with the others
 // (reloading the problem's slot tables), so the launch ends when every segment is drained -- no
 // per-problem launch tail, no side streams.
-template <int N, int WPB, class SP, bool HET = false>
-__global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const double* __restrict__ x0_all,
+//
+// MODE splits the solve over three launches (launch pipeline below) so that each one runs lean code:
+//   1  interior-point iterations only.  An instance that reaches its polish point is handed off --
+//      its active set (one bit per row slot and box row) and iteration count go to the work lists --
+//      and the group claims its next instance at once.  No polish code, no polish state.
+//   2  polish only, over the hand-off list: every instance runs the same fixed sequence (active-set
+//      factorization, solve, three refinements, acceptance test), so the four groups of a wave polish
+//      in lock-step instead of one at a time beside three iterating groups.  Rejected polishes go
+//      to the retry list.
+//   0  the complete algorithm in one kernel (iterations and polish interleaved per group): solves the
+//      retry list from scratch -- the arithmetic is deterministic, so this reproduces the rejected
+//      polish and carries on exactly as a single-kernel solve would -- and serves callers that bring
+//      their own instance lists or claim counter (closed loops, per-instance models, no-allocation entry).
+template <int N, int WPB, class SP, bool HET = false, int MODE = 0>
+__global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWork W, const double* __restrict__ x0_all,
                                                                const double* __restrict__ xref_all,
                                                                double* __restrict__ u_all, int64_t ld_u,
                                                                int32_t* __restrict__ status_all,
                                                                int32_t* __restrict__ iters_all, Settings S_all) {
+    static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
     constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
@@ -230,7 +244,22 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
     int32_t* __restrict__ status_out = status_all + seg0;
     int32_t* __restrict__ iters_out = iters_all ? iters_all + seg0 : nullptr;
     Settings S = S_all;
-    if (S.claim) S.claim += kRicClaimStride * seg;
+    if (W.cnt) {   // launch pipeline: this segment's counters and work lists (RicWork)
+        unsigned* wc = W.cnt + kRicClaimStride * seg;
+        if constexpr (MODE == 1) {
+            S.claim = wc + 0;
+        } else if constexpr (MODE == 2) {
+            S.index = W.pend_idx + seg0;
+            S.count = reinterpret_cast<const int32_t*>(wc + 1);
+            S.claim = wc + 2;
+        } else {
+            S.index = W.retry_idx + seg0;
+            S.count = reinterpret_cast<const int32_t*>(wc + 3);
+            S.claim = wc + 4;
+        }
+    } else if (S.claim) {
+        S.claim += kRicClaimStride * seg;
+    }
     if (kseg_i > 0) __syncthreads();   // every wave is done with the previous problem's tables
     if (batch <= 0) continue;
     const StageMats& MT = P.mats;
@@ -269,15 +298,72 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
     for (int sg = 0; sg < 2; ++sg) vb[sg] = &wv.vbox[g][own[sg] ? kseg[sg] - 1 : N][0];
 #define BX(F, sg, c) vb[sg][(F) * 2 + (c)]
-    bool rv[RS];
+    // Unused row slots are made inert instead of being masked: their coefficients are zero, w = 1,
+    // s = 1, z = 0, so every residual, direction and sum below gets an exact zero from them and the
+    // slot loops are straight-line code (no exec-mask region per slot).  The validity bits are only
+    // consulted where the instance is set up and in the polish acceptance test.
+    unsigned rvm = 0;
 #pragma unroll
-    for (int s = 0; s < RS; ++s) rv[s] = P.r_valid[s * G16 + j] != 0;
+    for (int s = 0; s < RS; ++s) rvm |= (P.r_valid[s * G16 + j] != 0 ? 1u : 0u) << s;
+    auto valid = [&](int s) { return ((rvm >> s) & 1u) != 0; };
     const int p = P.p;
     const int m_rows = p + (boxed ? 4 * N : 0);
     const double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
     const double idl = 1.0 / POLISH_DELTA;
 
     // ---- helpers ----------------------------------------------------------------------
+    // Row-slot loops.  Slots are visited pairwise -- slot i of segment 0, then slot i of segment 1 --
+    // for i below the problem's slots-per-segment count (wave-uniform: a scalar branch ahead of the
+    // pairs i >= kSegMin, none below).  The next slot's coefficients and w are loaded one slot ahead
+    // and a scheduling barrier closes every slot: the live set stays one slot wide instead of
+    // growing with however many slots the compiler chooses to interleave.
+    struct SlotIn { double2 c01, c23; double w, iv; };
+    auto ld_slot = [&](int s) __attribute__((always_inline)) {
+        SlotIn in;
+        in.c01 = sh.cf01[s * G16 + j];
+        in.c23 = sh.cf23[s * G16 + j];
+        in.w = wv.w[s][lane];
+        in.iv = 1.0;
+        if constexpr (HET) in.iv = P.het_ric_invn[hinst * (RS * G16) + s * G16 + j];
+        return in;
+    };
+    auto coef = [&](const SlotIn& in, double (&c)[4]) __attribute__((always_inline)) {
+        c[0] = in.c01.x; c[1] = in.c01.y; c[2] = in.c23.x; c[3] = in.c23.y;
+        if constexpr (HET) {   // raw template coefficients x this instance's 1/||G_r||
+#pragma unroll
+            for (int a2 = 0; a2 < 4; ++a2) c[a2] *= in.iv;
+        }
+    };
+    constexpr int kSegMin = 6;
+    const int rseg = P.rseg;
+    auto for_slots = [&](auto&& body) __attribute__((always_inline)) {
+        SlotIn cur = ld_slot(0);
+#pragma unroll
+        for (int q = 0; q < RS; ++q) {
+            const int i = q >> 1, s = (q & 1) * RSEG + i;
+            if (i >= kSegMin && i >= rseg) break;   // uniform; the remaining slots are unused in every lane
+            const int qn = q + 1 < RS ? q + 1 : q;
+            const SlotIn nxt = ld_slot((qn & 1) * RSEG + (qn >> 1));
+            body(s, cur);
+            __builtin_amdgcn_sched_barrier(0);
+            cur = nxt;
+        }
+    };
+    // the same visit without the loads (slot state in registers only)
+    auto for_used = [&](auto&& body) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < RS; ++q) {
+            const int i = q >> 1;
+            if (i >= kSegMin && i >= rseg) break;
+            body((q & 1) * RSEG + i);
+        }
+    };
+#define FOR_SLOTS_BEGIN                                                                        \
+    for_slots([&](const int s, const SlotIn& in) __attribute__((always_inline)) {              \
+        const int sg = s / RSEG;                                                               \
+        double c[4];                                                                           \
+        coef(in, c);
+#define FOR_SLOTS_END });
     auto cf = [&](int s, double (&c)[4]) {
         const double2 a = sh.cf01[s * G16 + j], b = sh.cf23[s * G16 + j];
         c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y;
@@ -834,23 +920,25 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
     bool live = slot < nlive;   // the group has an instance to work on
     int64_t inst = live && S.index ? (int64_t)S.index[slot] : slot;
     bool fresh = true;          // ... that still needs its initial point
-    double s_[RS], z_[RS], ra[RS];
+    double s_[RS], z_[RS];
     double xs[2][4];
     double bnorm = 1.0, qnorm = 1.0;
     int it = 0;
     bool polish_failed = false;
     // write the result of the current instance and move the group to its next one
-    auto finish = [&](int st, bool zero_u) {
+    auto finish = [&](int st, bool zero_u, bool write = true) {
+        if (write) {
 #pragma unroll
-        for (int sg = 0; sg < 2; ++sg)
-            if (own[sg]) {
-                const int t = kseg[sg] - 1;
-                u_out[inst * ld_u + 2 * t] = zero_u ? 0.0 : BX(F_U, sg, 0);
-                u_out[inst * ld_u + 2 * t + 1] = zero_u ? 0.0 : BX(F_U, sg, 1);
+            for (int sg = 0; sg < 2; ++sg)
+                if (own[sg]) {
+                    const int t = kseg[sg] - 1;
+                    u_out[inst * ld_u + 2 * t] = zero_u ? 0.0 : BX(F_U, sg, 0);
+                    u_out[inst * ld_u + 2 * t + 1] = zero_u ? 0.0 : BX(F_U, sg, 1);
+                }
+            if (j == 0) {
+                status_out[inst] = st;
+                if (iters_out) iters_out[inst] = it;
             }
-        if (j == 0) {
-            status_out[inst] = st;
-            if (iters_out) iters_out[inst] = it;
         }
         slot = S.claim ? claim() : slot + stride;
         live = slot < nlive;
@@ -868,6 +956,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
             }
             // this instance's data (HET) / the launch's problem
             const double *Ipw = P.pre_w0, *IpE = P.pre_E, *Irw = P.r_w0, *IrE = P.r_E, *Ihq = P.hq;
+            const double *IpEd = P.pre_Ed, *IrEd = P.r_Ed, *Igoal = P.goal;
+            // The problem's data never changes inside the instance loop, and the compiler would hoist
+            // the loads below out of it -- dozens of registers of copies held for the whole kernel,
+            // which pushes row state out to scratch memory.  Passing the pointers through an empty asm
+            // makes them opaque, so the loads stay here.
+            asm volatile("" : "+s"(Ipw), "+s"(IpE), "+s"(Irw), "+s"(IrE), "+s"(Ihq), "+s"(IpEd), "+s"(IrEd), "+s"(Igoal));
+            int ji = j;   // likewise the lane's index into them (per-slot address offsets would be kept otherwise)
+            asm volatile("" : "+v"(ji));
             if constexpr (HET) {
                 hinst = inst;
 #pragma unroll
@@ -884,16 +980,17 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
             for (int k = 0; k < NX; ++k) {
                 xv0[k] = x0[inst * NX + k];
-                xr[k] = xref ? xref[inst * NX + k] : P.goal[k];
+                xr[k] = xref ? xref[inst * NX + k] : Igoal[k];
             }
             // x0-only rows (G_r = 0): preconditions
             const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
             double bad = 0.0;
-            for (int r = j; r < P.npre; r += G16) {
+            if constexpr (MODE != 2)   // (handed-off instances have passed this test)
+            for (int r = ji; r < P.npre; r += G16) {
                 double v = Ipw[r];
 #pragma unroll
                 for (int k = 0; k < NX; ++k) v -= IpE[r * NX + k] * xv0[k];
-                if (P.pre_Ed) v -= P.pre_Ed[r] * dd;
+                if (IpEd) v -= IpEd[r] * dd;
                 bad = v < -PRE_TOL ? 1.0 : bad;
             }
             it = 0;
@@ -907,14 +1004,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                 for (int s = 0; s < RS; ++s) {
                     double v = 0.0;
-                    if (rv[s]) {
-                        const int e = s * G16 + j;
+                    if (valid(s)) {
+                        const int e = s * G16 + ji;
                         v = Irw[e];
 #pragma unroll
                         for (int k = 0; k < NX; ++k) v -= IrE[e * NX + k] * xv0[k];
-                        if (P.r_Ed) v -= P.r_Ed[e] * dd;
+                        if (IrEd) v -= IrEd[e] * dd;
                     }
-                    wv.w[s][lane] = v;
+                    wv.w[s][lane] = valid(s) ? v : 1.0;
                     bn = fmax(bn, fabs(v));
                 }
 #pragma unroll
@@ -940,6 +1037,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                         u0n = fmax(u0n, fabs(u0));
                     }
                 }
+                if constexpr (MODE != 2) {   // the polish starts from the active set alone
                 // xs = S u0 (u0 = clip(0, lb, ub); zero whenever the box contains 0)
                 if (row_max(u0n) > 0.0) {
 #pragma unroll
@@ -959,9 +1057,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                     const int sg = s / RSEG;
                     double c[4];
                     cf(s, c);
-                    s_[s] = rv[s] ? fmax(wv.w[s][lane] - dot4(c, xs[sg]), 1.0) : 1.0;
-                    z_[s] = rv[s] ? 1.0 : 0.0;
-                    ra[s] = 0.0;
+                    s_[s] = valid(s) ? fmax(wv.w[s][lane] - dot4(c, xs[sg]), 1.0) : 1.0;
+                    z_[s] = valid(s) ? 1.0 : 0.0;
+                }
                 }
                 bnorm = 1.0 + row_max(bn);
                 qnorm = 1.0 + row_max(qn);
@@ -974,20 +1072,20 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
             double mu = 0.0, rpn = 0.0, gun = 0.0, umax = 0.0, wz = 0.0, wzabs = 0.0;
             double lo = 0.0, scf = 0.0;
             bool polish = false;
-            if (active) {
+            // polish: the active set (rows with s < z) as a bit per slot, fixed when the polish factorizes;
+            // the polish loops test it instead of reading s and z (which they leave alone)
+            unsigned actm = 0;
+            auto act = [&](int s) { return ((actm >> s) & 1u) != 0; };
+            if (MODE != 2 && active) {
                 double lz[2][4], musum = -0.0;
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                     for (int a = 0; a < 4; ++a) lz[sg][a] = -0.0;
-#pragma unroll
-                for (int s = 0; s < RS; ++s) {
-                    const int sg = s / RSEG;
-                    double c[4];
-                    cf(s, c);
-                    const double w = wv.w[s][lane];
-                    const double gu = rv[s] ? dot4(c, xs[sg]) : 0.0;
-                    const double rp = rv[s] ? gu + s_[s] - w : 0.0;
+                FOR_SLOTS_BEGIN
+                    const double w = in.w;
+                    const double gu = dot4(c, xs[sg]);
+                    const double rp = gu + s_[s] - w;
                     rpn = fmax(rpn, fabs(rp));
                     gun = fmax(gun, fabs(gu));
                     musum = fma(s_[s], z_[s], musum);
@@ -995,7 +1093,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                     for (int a = 0; a < 4; ++a) lz[sg][a] = fma(z_[s], c[a], lz[sg][a]);
                     wz = fma(w, z_[s], wz);
                     wzabs = fma(fabs(w), z_[s], wzabs);
-                }
+                FOR_SLOTS_END
 #pragma unroll
                 for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
@@ -1087,10 +1185,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
             // B1: psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1}
             if constexpr (HET) {
                 if (active) adjoint_scalar();
-            } else {
+            } else if constexpr (MODE != 2) {
                 adjoint_mm();
             }
-            if (active) {
+            if (MODE != 2 && active) {
                 RT_MARK(2);
                 double rdn = 0.0, hun = 0.0, gzn = 0.0;
 #pragma unroll
@@ -1147,6 +1245,51 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                     active = false;
                     polish = false;
                 }
+                if constexpr (MODE == 1) {
+                    if (polish) {
+                        // hand the instance to the polish launch: active rows (s < z) and active box rows
+                        unsigned m = 0;
+                        for_used([&](const int s) __attribute__((always_inline)) { m |= (s_[s] < z_[s] ? 1u : 0u) << s; });
+#pragma unroll
+                        for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                            for (int c = 0; c < 2; ++c)
+                                if (own[sg] && boxed) {
+                                    m |= (BX(F_SU, sg, c) < BX(F_ZU, sg, c) ? 1u : 0u) << (16 + (sg * 2 + c) * 2);
+                                    m |= (BX(F_SL, sg, c) < BX(F_ZL, sg, c) ? 1u : 0u) << (17 + (sg * 2 + c) * 2);
+                                }
+                        W.pend_mask[(seg0 + inst) * G16 + j] = m;
+                        if (j == 0) {
+                            W.pend_it[seg0 + inst] = it;
+                            const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 1, 1u);
+                            W.pend_idx[seg0 + pos] = (int32_t)inst;
+                        }
+                        finish(0, false, false);
+                        active = false;
+                        polish = false;
+                    }
+                }
+            }
+            if constexpr (MODE == 1) polish = false;   // (compile-time fact for the code below)
+            if constexpr (MODE == 2) {
+                // the hand-off record replaces residuals and decisions
+                polish = true;
+                if (active) {
+                    const unsigned m = W.pend_mask[(seg0 + inst) * G16 + j];
+                    actm = m & 0xFFFFu;
+                    it = W.pend_it[seg0 + inst];
+#pragma unroll
+                    for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            // the polish only compares slack with multiplier: restore the outcome of the comparison
+                            const bool bu = (m >> (16 + (sg * 2 + c) * 2)) & 1u, bl = (m >> (17 + (sg * 2 + c) * 2)) & 1u;
+                            BX(F_SU, sg, c) = bu ? 0.0 : 1.0;
+                            BX(F_ZU, sg, c) = bu ? 1.0 : 0.0;
+                            BX(F_SL, sg, c) = bl ? 0.0 : 1.0;
+                            BX(F_ZL, sg, c) = bl ? 1.0 : 0.0;
+                        }
+                }
             }
             const bool any_polish = __any(polish);
             RT_MARK(3);
@@ -1166,21 +1309,19 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                     for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
                 }
-#pragma unroll
-                for (int s = 0; s < RS; ++s) {
-                    const int sg = s / RSEG;
-                    double c[4];
-                    cf(s, c);
-                    const double w = wv.w[s][lane];
+                FOR_SLOTS_BEGIN
+                    const double w = in.w;
                     double d, t;
                     if (polish) {
                         // b^x = -(Qbar S x + sum (yg - d ryg) c) at x = 0, yg = 0: ryg = w on active rows
-                        d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
+                        const bool on = MODE == 2 ? act(s) : s_[s] < z_[s];
+                        actm |= (on ? 1u : 0u) << s;
+                        d = on ? idl : 0.0;
                         t = d != 0.0 ? d * w : 0.0;
                     } else {
-                        d = rv[s] ? z_[s] * frcp(s_[s]) : 0.0;
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - w : 0.0;
-                        t = rv[s] ? (s_[s] * z_[s] - z_[s] * rp) * frcp(s_[s]) : 0.0;
+                        d = z_[s] * frcp(s_[s]);
+                        const double rp = dot4(c, xs[sg]) + s_[s] - w;
+                        t = (s_[s] * z_[s] - z_[s] * rp) * frcp(s_[s]);
                     }
 #pragma unroll
                     for (int a = 0; a < 4; ++a) {
@@ -1189,7 +1330,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                         for (int b = a; b < 4; ++b) Wa[sg][sym10(a, b)] = fma(da, c[b], Wa[sg][sym10(a, b)]);
                         acc[sg][a] = fma(t, c[a], acc[sg][a]);
                     }
-                }
+                FOR_SLOTS_END
                 // stage-N totals of W
                 double wn[10];
 #pragma unroll
@@ -1240,6 +1381,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
             // the refinement solve (k = 2 of a normal trip) only once mu <= REFINE_MU; before
             // that its correction is zero
             const bool refine = mu <= REFINE_MU;
+            double ra[RS];   // polish: multiplier estimates of the active rows (set at k = 0, live only in a polish trip)
 #pragma unroll
             for (int k = 0; k < POLISH_REFINE + 1; ++k) {
                 if (k == 3 && !any_polish) break;
@@ -1274,16 +1416,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                 wb();
                 if (polish) {
                     // update: yg += d (G dx - ryg); yu += dbu (dx - ryu); yl += dbl (-dx - ryl); x += dx
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
-                        const int sg = s / RSEG;
-                        double c[4];
-                        cf(s, c);
-                        const double d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
+                    FOR_SLOTS_BEGIN
+                        const double d = act(s) ? idl : 0.0;
                         // ryg of this solve: w - G x at the x before the update (x = 0 at k = 0)
-                        const double ryg = d != 0.0 ? wv.w[s][lane] - (k == 0 ? 0.0 : dot4(c, xvv[sg])) : 0.0;
+                        const double ryg = d != 0.0 ? in.w - (k == 0 ? 0.0 : dot4(c, xvv[sg])) : 0.0;
                         ra[s] = fma(d, dot4(c, dy[sg]) - ryg, k == 0 ? 0.0 : ra[s]);
-                    }
+                    FOR_SLOTS_END
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg) {
                         const int t = kseg[sg] - 1;
@@ -1309,18 +1447,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                         for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                             for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
-#pragma unroll
-                        for (int s = 0; s < RS; ++s) {
-                            const int sg = s / RSEG;
-                            double c[4];
-                            cf(s, c);
-                            const double d = (rv[s] && s_[s] < z_[s]) ? idl : 0.0;
+                        FOR_SLOTS_BEGIN
+                            const double d = act(s) ? idl : 0.0;
                             const double gx = dot4(c, xvv[sg]);
-                            const double ryg = d != 0.0 ? wv.w[s][lane] - gx : 0.0;
+                            const double ryg = d != 0.0 ? in.w - gx : 0.0;
                             const double t = -(ra[s] - d * ryg);
 #pragma unroll
                             for (int a = 0; a < 4; ++a) acc[sg][a] = fma(t, c[a], acc[sg][a]);
-                        }
+                        FOR_SLOTS_END
                         wb();
                         write_bx(acc, xvv, -1.0);
 #pragma unroll
@@ -1364,12 +1498,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                         if (P.r_partner) {
 #pragma unroll
                             for (int s = 0; s < RS; ++s)
-                                scr[s][lane] = (rv[s] && s_[s] < z_[s]) ? ra[s] : NAN;
+                                scr[s][lane] = act(s) ? ra[s] : NAN;
                             wb();
 #pragma unroll
                             for (int s = 0; s < RS; ++s) {
-                                const int pr = rv[s] ? sh.partner[s * G16 + j] : -1;
-                                paired[s] = pr >= 0 && s_[s] < z_[s] &&
+                                const int pr = sh.partner[s * G16 + j];   // -1 in unused slots
+                                paired[s] = pr >= 0 && act(s) &&
                                             !isnan(scr[pr / G16][(lane & 48) + (pr % G16)]);
                             }
                             wb();
@@ -1377,7 +1511,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                         for (int s = 0; s < RS; ++s) {
                             const int sg = s / RSEG;
-                            if (rv[s]) {
+                            if (valid(s)) {
                                 double c[4];
                                 cf(s, c);
                                 const double w = wv.w[s][lane];
@@ -1401,6 +1535,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                                 }
                             finish(CARMPC_OPTIMAL, false);
                             active = false;
+                        } else if constexpr (MODE == 2) {
+                            // rejected: the single-kernel launch solves the instance again from the start
+                            if (j == 0) {
+                                const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 3, 1u);
+                                W.retry_idx[seg0 + pos] = (int32_t)inst;
+                            }
+                            finish(0, false, false);
+                            active = false;
                         }
                         polish_failed = true;
                     }
@@ -1414,16 +1556,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                 if (k == 0) {
                     double amax = INFINITY, mua = -0.0;
                     double dsv[RS], dzv[RS];
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
-                        const int sg = s / RSEG;
-                        double c[4];
-                        cf(s, c);
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
-                        dsv[s] = rv[s] ? -rp - dot4(c, dy[sg]) : 0.0;
-                        dzv[s] = rv[s] ? (-s_[s] * z_[s] - z_[s] * dsv[s]) * frcp(s_[s]) : 0.0;
+                    FOR_SLOTS_BEGIN
+                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
+                        dsv[s] = -rp - dot4(c, dy[sg]);
+                        dzv[s] = (-s_[s] * z_[s] - z_[s] * dsv[s]) * frcp(s_[s]);
                         amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
-                    }
+                    FOR_SLOTS_END
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
@@ -1446,8 +1584,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                             }
                         }
                     const double a = fmin(1.0, row_min(amax));
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) mua = fma(fma(a, dsv[s], s_[s]), fma(a, dzv[s], z_[s]), mua);
+                    for_used([&](const int s) __attribute__((always_inline)) {
+                        mua = fma(fma(a, dsv[s], s_[s]), fma(a, dzv[s], z_[s]), mua);
+                    });
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
@@ -1467,17 +1606,13 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
-                        const int sg = s / RSEG;
-                        double c[4];
-                        cf(s, c);
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
+                    FOR_SLOTS_BEGIN
+                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
                         const double rc = s_[s] * z_[s] + dsv[s] * dzv[s] - smu;
-                        const double t = rv[s] ? (rc - z_[s] * rp) * frcp(s_[s]) : 0.0;
+                        const double t = (rc - z_[s] * rp) * frcp(s_[s]);   // unused slot: finite, times c = 0
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(t, c[aa], acc[sg][aa]);
-                    }
+                    FOR_SLOTS_END
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
@@ -1515,20 +1650,16 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
                     if (refine)
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
-                        const int sg = s / RSEG;
-                        double c[4];
-                        cf(s, c);
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
+                    FOR_SLOTS_BEGIN
+                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
                         const double dsa = -rp - dot4(c, dyA[sg]);
                         const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
                         const double rc = s_[s] * z_[s] + dsa * dza - smu;
                         const double ds = -rp - dot4(c, dy[sg]);
-                        const double dz = rv[s] ? (-rc - z_[s] * ds) * frcp(s_[s]) : 0.0;
+                        const double dz = (-rc - z_[s] * ds) * frcp(s_[s]);   // unused slot: smu, times c = 0
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(-dz, c[aa], acc[sg][aa]);
-                    }
+                    FOR_SLOTS_END
                     wb();
                     if (refine) write_bx(acc, dy, -1.0);
 #pragma unroll
@@ -1572,19 +1703,17 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
 #pragma unroll
                         for (int aa = 0; aa < 4; ++aa) dyT[sg][aa] = xvv[sg][aa] + dy[sg][aa];
                     double amax = INFINITY, dsv[RS], dzv[RS];
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
-                        const int sg = s / RSEG;
-                        double c[4];
-                        cf(s, c);
-                        const double rp = rv[s] ? dot4(c, xs[sg]) + s_[s] - wv.w[s][lane] : 0.0;
+                    FOR_SLOTS_BEGIN
+                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
                         const double dsa = -rp - dot4(c, dyA[sg]);
                         const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
-                        const double rc = s_[s] * z_[s] + dsa * dza - smu;
-                        dsv[s] = rv[s] ? -rp - dot4(c, dyT[sg]) : 0.0;
-                        dzv[s] = rv[s] ? (-rc - z_[s] * dsv[s]) * frcp(s_[s]) : 0.0;
+                        // the centering term belongs to rows with a multiplier (z > 0 on every used
+                        // slot, z = 0 on unused ones, which must keep dz = 0)
+                        const double rc = s_[s] * z_[s] + dsa * dza - (z_[s] > 0.0 ? smu : 0.0);
+                        dsv[s] = -rp - dot4(c, dyT[sg]);
+                        dzv[s] = (-rc - z_[s] * dsv[s]) * frcp(s_[s]);
                         amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
-                    }
+                    FOR_SLOTS_END
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
@@ -1606,11 +1735,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, const 
                             }
                         }
                     const double a = fmin(1.0, STEP_FRAC * row_min(amax));
-#pragma unroll
-                    for (int s = 0; s < RS; ++s) {
+                    for_used([&](const int s) __attribute__((always_inline)) {
                         s_[s] = fma(a, dsv[s], s_[s]);
                         z_[s] = fma(a, dzv[s], z_[s]);
-                    }
+                    });
 #pragma unroll
                     for (int sg = 0; sg < 2; ++sg) {
 #pragma unroll
@@ -1652,8 +1780,8 @@ bool riccati_supported_N(int N) { return N == 10 || N == 20; }
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
 template <class Kern>
-hipError_t ric_launch(Kern kern, const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out,
-                      int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
+hipError_t ric_launch(Kern kern, const RicSegs& T, const RicWork& W, int64_t total, const double* x0, const double* xref,
+                      double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
     constexpr int WPB = 4;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -1666,19 +1794,21 @@ hipError_t ric_launch(Kern kern, const RicSegs& T, int64_t total, const double* 
     const int64_t per_block = (int64_t)WPB * 4;
     int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, (total + per_block - 1) / per_block);
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, T, x0, xref, u_out, ld_u, status, iters, s);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, T, W, x0, xref, u_out, ld_u, status, iters, s);
     return hipGetLastError();
 }
-template <bool HET>
-hipError_t ric_dispatch(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
-                        int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
+template <bool HET, int MODE>
+hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const double* x0, const double* xref,
+                        double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
+                        int* unsupported) {
     constexpr int WPB = 4;
     const bool bike = T.P[0].ric == 2;
     if (HET && !bike) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
-#define RIC_GO(NN, MODEL) ric_launch(ipm_riccati_kernel<NN, WPB, MODEL, HET>, T, total, x0, xref, u_out, ld_u, status, iters, s, stream)
+#define RIC_GO(NN, MODEL) \
+    ric_launch(ipm_riccati_kernel<NN, WPB, MODEL, HET, MODE>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
     switch (T.P[0].N) {
         case 10: return bike ? RIC_GO(10, BicycleModel) : RIC_GO(10, DenseModel);
         case 20: return bike ? RIC_GO(20, BicycleModel) : RIC_GO(20, DenseModel);
@@ -1686,6 +1816,32 @@ hipError_t ric_dispatch(const RicSegs& T, int64_t total, const double* x0, const
     }
 #undef RIC_GO
 }
+
+// The launch pipeline: iterations with hand-off, lock-step polish, single-kernel solve of the rejected
+// polishes (see MODE at the kernel).  Work lists and counters live for the call, stream-ordered.  The
+// third launch usually finds an empty list; its workgroups read the count and return.
+hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
+                        int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
+    const size_t n = (size_t)total, ncnt = (size_t)kRicClaimStride * kRicMaxSeg;
+    const size_t bytes = sizeof(unsigned) * ncnt + sizeof(int32_t) * 3 * n + sizeof(uint32_t) * kRicLanes * n;
+    char* base = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&base), bytes, stream);
+    if (e != hipSuccess) return e;
+    RicWork W{};
+    W.cnt = reinterpret_cast<unsigned*>(base);
+    W.pend_idx = reinterpret_cast<int32_t*>(W.cnt + ncnt);
+    W.pend_it = W.pend_idx + n;
+    W.retry_idx = W.pend_it + n;
+    W.pend_mask = reinterpret_cast<uint32_t*>(W.retry_idx + n);
+    e = launch_zero_u32(W.cnt, (int)ncnt, stream);
+    if (e == hipSuccess) e = ric_dispatch<false, 1>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (e == hipSuccess) e = ric_dispatch<false, 2>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (e == hipSuccess) e = ric_dispatch<false, 0>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    const hipError_t ef = hipFreeAsync(base, stream);
+    return e != hipSuccess ? e : ef;
+}
+// callers with their own instance list or claim counter get the single kernel
+bool ric_wants_pipeline(const Settings& s, int64_t total) { return !s.index && !s.count && !s.claim && total > 1; }
 }  // namespace
 
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
@@ -1702,19 +1858,23 @@ hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, 
     T.off[0] = 0;
     T.off[1] = batch;
     T.P[0] = P;
+    if (!het && ric_wants_pipeline(s, batch) && riccati_supported_N(P.N))
+        return ric_pipeline(T, batch, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     // per-launch claim counter, stream-ordered (allocated, zeroed, freed on `stream`)
+    const RicWork none{};
     return launch_with_claim(s, batch, stream, [&](const Settings& sc) {
-        return het ? ric_dispatch<true>(T, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported)
-                   : ric_dispatch<false>(T, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported);
+        return het ? ric_dispatch<true, 0>(T, none, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported)
+                   : ric_dispatch<false, 0>(T, none, batch, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported);
     });
 }
 
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                                int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
     *unsupported = 0;
-    static_assert(sizeof(RicSegs) + 6 * sizeof(void*) + sizeof(Settings) + 64 <= 4096, "kernel arguments exceed 4 KB");
+    static_assert(sizeof(RicSegs) + sizeof(RicWork) + 6 * sizeof(void*) + sizeof(Settings) + 64 <= 4096,
+                  "kernel arguments exceed 4 KB");
     const int nseg = T.nseg;
-    if (nseg < 1 || nseg > kRicMaxSeg || !s.claim) {
+    if (nseg < 1 || nseg > kRicMaxSeg) {
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
@@ -1725,7 +1885,14 @@ hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double*
         }
     const int64_t total = T.off[nseg] - T.off[0];
     if (total <= 0) return hipSuccess;
-    return ric_dispatch<false>(T, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (ric_wants_pipeline(s, total))
+        return ric_pipeline(T, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (!s.claim) {   // a single kernel over several segments claims from one counter per segment
+        *unsupported = 1;
+        return hipErrorInvalidValue;
+    }
+    const RicWork none{};
+    return ric_dispatch<false, 0>(T, none, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
 }
 
 }  // namespace carmpc
