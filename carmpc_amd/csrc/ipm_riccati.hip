@@ -73,7 +73,7 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #endif
 // Stages of read-ahead of the matrix-core passes (see the comment at kPre).
 #ifndef CARMPC_RIC_KPRE
-#define CARMPC_RIC_KPRE 3
+#define CARMPC_RIC_KPRE 1
 #endif
 #ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
                                 // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
