@@ -280,18 +280,26 @@ struct RicSegs {
     int64_t off[kRicMaxSeg + 1];
     DevProblem P[kRicMaxSeg];
 };
-// Work lists of the Riccati launch pipeline (ipm_riccati.hip: iterations -> polish -> retry), device
-// memory for one call.  cnt holds kRicClaimStride words per segment: [0] claim counter of the iteration
-// launch, [1] number of handed-off instances, [2] claim counter of the polish launch, [3] number of
-// rejected polishes, [4] claim counter of the retry launch.  The index lists are per segment, starting at
-// the segment's first instance; masks and iteration counts are stored per instance.  All null: no pipeline.
+// Work lists of the Riccati launch pipeline (ipm_riccati.hip: rounds of iterations -> polish, then the
+// single kernel), device memory for one call.  cnt holds kRicClaimStride words per segment: [0] claim
+// counter of round 0's iteration launch; for round r: [4r+1] number of handed-off instances, [4r+2]
+// claim counter of the polish launch, [4r+3] number of rejected polishes, [4r+4] claim counter of the
+// launch that takes them (round r+1's iterations, or the single kernel after the last round).  The index
+// lists are per segment, starting at the segment's first instance, and reused from round to round;
+// masks and iteration counts are stored per instance.  cnt null: no pipeline.
 struct RicWork {
     unsigned* cnt;
     int32_t* pend_idx;    // total: segment-relative rows awaiting the polish
     int32_t* pend_it;     // total: IPM iterations done at the hand-off
     int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
     uint32_t* pend_mask;  // total x 16 lanes: bit s = row slot s active, bits 16.. = box rows of the owned inputs
+    int32_t round;        // pipeline round of this launch
 };
+// One round measured best on the 131,072-instance mixed shard (11.45M QP/s; two rounds 10.9M): some 6 %
+// of the polishes are rejected, a second round solves those again with the lean kernels but still leaves
+// a latency-bound single-kernel tail for the ones rejected twice.
+constexpr int kRicRounds = 1;
+static_assert(4 * kRicRounds < kRicClaimStride, "counter slots per segment");
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                                int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported);
 

@@ -244,18 +244,24 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     int32_t* __restrict__ status_out = status_all + seg0;
     int32_t* __restrict__ iters_out = iters_all ? iters_all + seg0 : nullptr;
     Settings S = S_all;
-    if (W.cnt) {   // launch pipeline: this segment's counters and work lists (RicWork)
+    if (W.cnt) {   // launch pipeline: this segment's counters and work lists of round W.round (RicWork)
         unsigned* wc = W.cnt + kRicClaimStride * seg;
         if constexpr (MODE == 1) {
-            S.claim = wc + 0;
+            if (W.round == 0) {
+                S.claim = wc + 0;
+            } else {   // the previous round's rejected polishes
+                S.index = W.retry_idx + seg0;
+                S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
+                S.claim = wc + 4 * W.round;
+            }
         } else if constexpr (MODE == 2) {
             S.index = W.pend_idx + seg0;
-            S.count = reinterpret_cast<const int32_t*>(wc + 1);
-            S.claim = wc + 2;
-        } else {
+            S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round + 1);
+            S.claim = wc + 4 * W.round + 2;
+        } else {   // after the last round
             S.index = W.retry_idx + seg0;
-            S.count = reinterpret_cast<const int32_t*>(wc + 3);
-            S.claim = wc + 4;
+            S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
+            S.claim = wc + 4 * W.round;
         }
     } else if (S.claim) {
         S.claim += kRicClaimStride * seg;
@@ -923,7 +929,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     double s_[RS], z_[RS];
     double xs[2][4];
     double bnorm = 1.0, qnorm = 1.0;
-    int it = 0;
+    int it = 0, npol = 0;   // iterations; polish points passed over (pipeline rounds > 0)
     bool polish_failed = false;
     // write the result of the current instance and move the group to its next one
     auto finish = [&](int st, bool zero_u, bool write = true) {
@@ -994,6 +1000,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 bad = v < -PRE_TOL ? 1.0 : bad;
             }
             it = 0;
+            npol = 0;
             polish_failed = false;
             if (row_max(bad) > 0.0) {
                 finish(CARMPC_PRIMAL_INFEASIBLE, true);
@@ -1234,6 +1241,15 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     const bool res_ok = rpn <= S.tol * pscale && rdn <= S.tol * dscale;
                     const bool last = it >= S.max_iter;
                     polish = !polish_failed && ((res_ok && mu <= POLISH_MU) || last);
+                    if constexpr (MODE == 1) {
+                        // round r of the pipeline: the instance's first r polishes are known to be rejected
+                        // (that is why it is here); pass them over the way the single kernel carries on
+                        // after a rejection -- same iterate, no polish until a step has been taken
+                        if (polish && npol < W.round) {
+                            ++npol;
+                            polish = false;
+                        }
+                    }
                     if (!polish) {
                         if (last) done = CARMPC_MAX_ITER;
                         else if (res_ok && mu <= S.tol_mu) done = CARMPC_OPTIMAL;
@@ -1261,7 +1277,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         W.pend_mask[(seg0 + inst) * G16 + j] = m;
                         if (j == 0) {
                             W.pend_it[seg0 + inst] = it;
-                            const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 1, 1u);
+                            const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);
                             W.pend_idx[seg0 + pos] = (int32_t)inst;
                         }
                         finish(0, false, false);
@@ -1538,7 +1554,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         } else if constexpr (MODE == 2) {
                             // rejected: the single-kernel launch solves the instance again from the start
                             if (j == 0) {
-                                const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 3, 1u);
+                                const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 3, 1u);
                                 W.retry_idx[seg0 + pos] = (int32_t)inst;
                             }
                             finish(0, false, false);
@@ -1817,9 +1833,9 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
 #undef RIC_GO
 }
 
-// The launch pipeline: iterations with hand-off, lock-step polish, single-kernel solve of the rejected
-// polishes (see MODE at the kernel).  Work lists and counters live for the call, stream-ordered.  The
-// third launch usually finds an empty list; its workgroups read the count and return.
+// The launch pipeline: rounds of iterations with hand-off and lock-step polish, then the single kernel for
+// what the last round rejected (see MODE at the kernel).  Work lists and counters live for the call,
+// stream-ordered.  The last launch usually finds an empty list; its workgroups read the count and return.
 hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                         int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
     const size_t n = (size_t)total, ncnt = (size_t)kRicClaimStride * kRicMaxSeg;
@@ -1834,8 +1850,12 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
     W.retry_idx = W.pend_it + n;
     W.pend_mask = reinterpret_cast<uint32_t*>(W.retry_idx + n);
     e = launch_zero_u32(W.cnt, (int)ncnt, stream);
-    if (e == hipSuccess) e = ric_dispatch<false, 1>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
-    if (e == hipSuccess) e = ric_dispatch<false, 2>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    // rounds of (iterations, polish): round r takes the instances whose first r polishes were rejected
+    // (a few per cent after round 0); what is left after the last round goes to the single kernel
+    for (W.round = 0; W.round < kRicRounds && e == hipSuccess; ++W.round) {
+        e = ric_dispatch<false, 1>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+        if (e == hipSuccess) e = ric_dispatch<false, 2>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    }
     if (e == hipSuccess) e = ric_dispatch<false, 0>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     const hipError_t ef = hipFreeAsync(base, stream);
     return e != hipSuccess ? e : ef;
