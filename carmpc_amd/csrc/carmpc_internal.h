@@ -299,6 +299,9 @@ struct RicWork {
 // of the polishes are rejected, a second round solves those again with the lean kernels but still leaves
 // a latency-bound single-kernel tail for the ones rejected twice.
 constexpr int kRicRounds = 1;
+// smallest batch (instances of one call) solved by the pipeline: measured cross-over between 32,768 (single
+// kernel 8.5M QP/s, pipeline 8.2M) and 65,536 (9.1M, 9.8M) on RoadOneCarEnv, N = 20
+constexpr int kRicPipelineMin = 49152;
 static_assert(4 * kRicRounds < kRicClaimStride, "counter slots per segment");
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                                int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported);

@@ -22,6 +22,7 @@
 #include "lanes.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include <hip/hip_runtime.h>
@@ -1241,11 +1242,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     const bool res_ok = rpn <= S.tol * pscale && rdn <= S.tol * dscale;
                     const bool last = it >= S.max_iter;
                     polish = !polish_failed && ((res_ok && mu <= POLISH_MU) || last);
-                    if constexpr (MODE == 1) {
-                        // round r of the pipeline: the instance's first r polishes are known to be rejected
-                        // (that is why it is here); pass them over the way the single kernel carries on
-                        // after a rejection -- same iterate, no polish until a step has been taken
-                        if (polish && npol < W.round) {
+                    if constexpr (MODE != 2) {
+                        // round r of the pipeline (the single kernel after the last round included): the
+                        // instance's first r polishes are known to be rejected -- that is why it is here;
+                        // pass them over the way the single kernel carries on after a rejection: same
+                        // iterate, no polish until a step has been taken
+                        if (W.cnt && polish && npol < W.round) {
                             ++npol;
                             polish = false;
                         }
@@ -1860,8 +1862,16 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
     const hipError_t ef = hipFreeAsync(base, stream);
     return e != hipSuccess ? e : ef;
 }
-// callers with their own instance list or claim counter get the single kernel
-bool ric_wants_pipeline(const Settings& s, int64_t total) { return !s.index && !s.count && !s.claim && total > 1; }
+// Callers with their own instance list (closed loops: live slots, few per step) or claim counter (the
+// no-allocation entry) get the single kernel, and so do small batches: the pipeline's last launch has
+// the latency of one complete solve however few instances it holds.
+bool ric_wants_pipeline(const Settings& s, int64_t total) {
+    static const long long min_total = [] {
+        const char* v = getenv("CARMPC_RIC_PIPELINE_MIN");   // experiment switch
+        return v ? atoll(v) : (long long)kRicPipelineMin;
+    }();
+    return !s.index && !s.count && !s.claim && total >= min_total;
+}
 }  // namespace
 
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref, double* u_out,
@@ -1907,12 +1917,19 @@ hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double*
     if (total <= 0) return hipSuccess;
     if (ric_wants_pipeline(s, total))
         return ric_pipeline(T, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
-    if (!s.claim) {   // a single kernel over several segments claims from one counter per segment
-        *unsupported = 1;
-        return hipErrorInvalidValue;
-    }
+    // a single kernel over several segments claims from one counter per segment (kRicClaimStride words apart)
     const RicWork none{};
-    return ric_dispatch<false, 0>(T, none, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    if (s.claim) return ric_dispatch<false, 0>(T, none, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
+    unsigned* counters = nullptr;
+    const int ncnt = kRicClaimStride * nseg;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&counters), sizeof(unsigned) * ncnt, stream);
+    if (e != hipSuccess) return e;
+    Settings sc = s;
+    sc.claim = counters;
+    e = launch_zero_u32(counters, ncnt, stream);
+    if (e == hipSuccess) e = ric_dispatch<false, 0>(T, none, total, x0, xref, u_out, ld_u, status, iters, sc, stream, unsupported);
+    const hipError_t ef = hipFreeAsync(counters, stream);
+    return e != hipSuccess ? e : ef;
 }
 
 }  // namespace carmpc

@@ -1,0 +1,41 @@
+"""The Riccati solve as a launch pipeline (iterations with hand-off -> lock-step polish -> single
+kernel for the rejected polishes; batches of 49,152 instances and more) against the same solve in
+ONE kernel.  carmpc_solve_batch_noalloc always runs the single kernel (it brings its own claim
+counter), so the two entry points give the two paths on identical inputs: statuses and iteration
+counts must be equal, u to 1e-12 (both paths run the same arithmetic per instance; the pipeline
+only changes which launch performs which part)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import TERMINAL_SETS
+from test_zz_no_alloc import _call, _x0
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("env,N", [("RoadMultipleCarsEnv", 20), ("RoadEnv", 20), ("RoadOneCarEnv", 10)])
+def test_pipeline_equals_single_kernel(gpu_available, env, N):
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd import _native
+    from carmpc_amd.qp import QPProblem, SolverSettings
+    lib = _native.load()
+    asm = oa.build(env, N, terminal_set_dir=TERMINAL_SETS)
+    qp = QPProblem(N=N, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    assert qp.kernel == 7
+    B = 65536
+    X = torch.as_tensor(_x0(np.random.default_rng(11), asm.goal[0], B)).to(qp.device)
+    settings = SolverSettings()
+    u1, st1, it1 = _call(lib.carmpc_solve_batch, qp, X, settings)            # pipeline
+    u0, st0, it0 = _call(lib.carmpc_solve_batch_noalloc, qp, X, settings)    # single kernel
+    torch.cuda.synchronize()
+    assert int((st1 < 0).sum()) == 0                                         # every instance got a result
+    assert torch.equal(st1, st0) and torch.equal(it1, it0)
+    ok = (st0 == 0).cpu().numpy()
+    assert ok.sum() > B // 8
+    np.testing.assert_allclose(u1.cpu().numpy()[ok], u0.cpu().numpy()[ok], rtol=0, atol=1e-12)
+    assert torch.equal(u1[st1 != 0], u0[st1 != 0])                           # (infeasible instances: last iterate or zeros)
