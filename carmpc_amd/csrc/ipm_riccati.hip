@@ -731,19 +731,30 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     const int oBU1 = mr == 1 ? O_BU : O_ZERO;                  // b^u_0 in row 1 (for E b^u)
     const int oKPt = m_top ? O_DB + mr : O_ZERO;               // kappa in rows 0-1
     const int oDrow = O_CH + (mr == 0 ? 1 : 2);                // 1/p0 in row 0, 1/p1 below
-    double cA = 0.0, cAT = 0.0, cBp = 0.0, cBpT = 0.0, cB0r = 0.0, cB1r = 0.0, cB0m1 = 0.0, cQ = 0.0, cPt = 0.0;
+    double cA = 0.0, cBp = 0.0, cB0r = 0.0, cB1r = 0.0, cQ = 0.0, cPt = 0.0;
     if constexpr (!HET) {
         cA = MT.A[mr * 4 + mc];                       // A^
-        cAT = MT.A[mc * 4 + mr];                      // (A')^
         cBp = m_left ? MT.B[mr * 2 + mc] : 0.0;       // [B 0 0]^
-        cBpT = m_top ? MT.B[mc * 2 + mr] : 0.0;       // [B 0 0]'^
         cB0r = MT.B[mr * 2];                          // column 0 of B in every column
         cB1r = MT.B[mr * 2 + 1];                      // column 1 of B in every column
-        cB0m1 = mc == 1 ? cB0r : 0.0;
         cQ = MT.Q[mr * 4 + mc];
         cPt = MT.P[mr * 4 + mc];
     }
-    const double k10 = (mr == 1 && mc == 0) ? 1.0 : 0.0, kd = (mr == mc && m_top) ? 1.0 : 0.0;
+    // Constants that only one kind of pass needs are rebuilt at its start (a dozen instructions, or two
+    // matrix-core transposes) instead of occupying registers through the row phases; the lane index goes
+    // through an empty asm so that the compiler does not hoist them back out of the trip loop.
+    struct PassK { double cB0m1, k10, kd, cI; };
+    auto pass_consts = [&]() __attribute__((always_inline)) {
+        int lz = lane;
+        asm volatile("" : "+v"(lz));
+        const int r_ = lz >> 4, c_ = lz & 3;
+        PassK k;
+        k.cB0m1 = c_ == 1 ? cB0r : 0.0;                          // column 0 of B in column 1
+        k.k10 = (r_ == 1 && c_ == 0) ? 1.0 : 0.0;
+        k.kd = (r_ == c_ && r_ < 2) ? 1.0 : 0.0;                 // identity of the leading 2x2 block
+        k.cI = r_ == c_ ? 1.0 : 0.0;
+        return k;
+    };
     // One wave per SIMD leaves nothing to hide an LDS round trip (~70 cycles) or an MFMA result
     // (28 cycles to a dependent MFMA, 16 cycles of pipe each) behind, so the passes are software
     // pipelined by hand: stage t's record fields are read kPre stages ahead, side products and
@@ -783,6 +794,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // broadcast).  K_t -> rec[t][0..7], (l, 1/p0, 1/p1) -> rec[t][8..10], kappa_t -> rec[t][18..19]
     auto factor_mm = [&]() {
         wb();
+        const PassK pk = pass_consts();
+        const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
         struct In { double db0, db1, buT, bu01, Wt, bxv; };
         struct Out { double En, Z, zg, l, drow; };
         In in[N];
@@ -847,6 +860,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // factored form above, p_t = b^x_t + A'p_{t+1} - K_t'g_t
     auto back_mm = [&]() {
         wb();
+        const PassK pk = pass_consts();
+        const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
         struct In { double buT, bu01, l, drow, K, bxv; };
         In in[N];
         double En[N], zg[N];
@@ -883,6 +898,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // forward pass: v_t = kappa_t - K_t y_t -> rec[t][16..17]; y_{t+1} = A y_t + B v_t -> rec[t][12..15]
     auto forward_mm = [&]() {
         wb();
+        const PassK pk = pass_consts();
+        const double cAT = mm(cA, pk.cI, 0.0), cBpT = mm(cBp, pk.cI, 0.0);   // (A')^ and [B 0 0]'^
         double KT[N], kp[N], y[N + 1], v[N];
         y[0] = 0.0;
 #pragma unroll
