@@ -45,6 +45,7 @@ def _stale(obj, src, cmd):
             return True
     deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h"),
             os.path.join(REPO, "include", "carmpc.h")]
+    deps += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".inc")]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 

@@ -766,7 +766,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     auto stage_fence = [] { __builtin_amdgcn_sched_barrier(0); };
     // adjoint pass: psi_k = lam_k + A'psi_{k+1} for lamZ (column 0) and lamH (column 1);
     // gz_t, hs_t = B'psi_{t+1} -> rec[t][12..15]
-    auto adjoint_mm = [&]() {
+    auto adjoint_mm = [&]() __attribute__((always_inline)) {
         wb();
         double lam[N], psi[N + 1], gh[N];
         psi[N] = 0.0;
@@ -792,7 +792,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // explicit inverse stalled the IPM on such instances).  The three entries of Re_t come out of
     // MFMAs with B's columns replicated, so every lane of the block holds them (no cross-lane
     // broadcast).  K_t -> rec[t][0..7], (l, 1/p0, 1/p1) -> rec[t][8..10], kappa_t -> rec[t][18..19]
-    auto factor_mm = [&]() {
+    auto factor_mm = [&]() __attribute__((always_inline)) {
         wb();
         const PassK pk = pass_consts();
         const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
@@ -858,7 +858,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     };
     // backward linear pass with the stored factor: kappa_t = Re_t^{-1}(b^u_t + B'p_{t+1}) in the
     // factored form above, p_t = b^x_t + A'p_{t+1} - K_t'g_t
-    auto back_mm = [&]() {
+    auto back_mm = [&]() __attribute__((always_inline)) {
         wb();
         const PassK pk = pass_consts();
         const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
@@ -896,7 +896,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
         wb();
     };
     // forward pass: v_t = kappa_t - K_t y_t -> rec[t][16..17]; y_{t+1} = A y_t + B v_t -> rec[t][12..15]
-    auto forward_mm = [&]() {
+    auto forward_mm = [&]() __attribute__((always_inline)) {
         wb();
         const PassK pk = pass_consts();
         const double cAT = mm(cA, pk.cI, 0.0), cBpT = mm(cBp, pk.cI, 0.0);   // (A')^ and [B 0 0]'^
@@ -1328,479 +1328,37 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             }
             const bool any_polish = __any(polish);
             RT_MARK(3);
-            if (!__any(active)) continue;
-            // ================= factorization rows (R2) + first right-hand side =================
-            // normal: d = z/s, predictor rhs; polish: d = 1/delta on the active set (s < z)
-            // per owned input: normal e1..e4 = dsu, dzu, dsl, dzl of the direction, vx = du;
-            // polish vx = x, e1 = yu, e2 = yl.  xvv: normal S du (corrector), polish S x.
-            double xvv[2][4], dyA[2][4];
-            double smu = 0.0;
-            if (active) {
-                double Wa[2][10], acc[2][4];
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg) {
-#pragma unroll
-                    for (int e = 0; e < 10; ++e) Wa[sg][e] = -0.0;
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
+            if constexpr (HET) {
+                // per-instance models: both forms interleaved per group (flags per lane)
+                if (!__any(active)) continue;
+#define RIC_GO active
+#define RIC_POLISH polish
+#define RIC_ANY_POLISH any_polish
+#include "ipm_riccati_solve.inc"
+#undef RIC_GO
+#undef RIC_POLISH
+#undef RIC_ANY_POLISH
+            } else {
+                // Shared model: the rest of the trip exists in two compile-time forms, the interior-point step and the
+                // active-set polish.  The single kernel (MODE 0) runs the polish form first for the groups that polish
+                // in this trip, then the step form for the others: each form keeps only its own vectors live, where
+                // code that interleaves them per group keeps the union (and spilled to scratch).  MODE 1 / 2
+                // instantiate one form each.
+                auto solve_phase = [&](auto pol_c, bool go) __attribute__((always_inline)) {
+                    constexpr bool POL = decltype(pol_c)::value;
+                    if (!__any(go)) return;
+#define RIC_GO go
+#define RIC_POLISH POL
+#define RIC_ANY_POLISH POL
+#include "ipm_riccati_solve.inc"
+#undef RIC_GO
+#undef RIC_POLISH
+#undef RIC_ANY_POLISH
+                };
+                if constexpr (MODE != 1) {
+                    if (any_polish) solve_phase(std::true_type{}, active && polish);
                 }
-                FOR_SLOTS_BEGIN
-                    const double w = in.w;
-                    double d, t;
-                    if (polish) {
-                        // b^x = -(Qbar S x + sum (yg - d ryg) c) at x = 0, yg = 0: ryg = w on active rows
-                        const bool on = MODE == 2 ? act(s) : s_[s] < z_[s];
-                        actm |= (on ? 1u : 0u) << s;
-                        d = on ? idl : 0.0;
-                        t = d != 0.0 ? d * w : 0.0;
-                    } else {
-                        d = z_[s] * frcp(s_[s]);
-                        const double rp = dot4(c, xs[sg]) + s_[s] - w;
-                        t = (s_[s] * z_[s] - z_[s] * rp) * frcp(s_[s]);
-                    }
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        const double da = d * c[a];
-#pragma unroll
-                        for (int b = a; b < 4; ++b) Wa[sg][sym10(a, b)] = fma(da, c[b], Wa[sg][sym10(a, b)]);
-                        acc[sg][a] = fma(t, c[a], acc[sg][a]);
-                    }
-                FOR_SLOTS_END
-                // stage-N totals of W
-                double wn[10];
-#pragma unroll
-                for (int e = 0; e < 10; ++e) wn[e] = row_sum((isN[0] ? Wa[0][e] : 0.0) + (isN[1] ? Wa[1][e] : 0.0));
-                double zero4[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-                wb();
-                write_bx(acc, zero4, 0.0);
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg) {
-                    const int t = kseg[sg] - 1;
-                    const int r = t * REC;
-                    double db[2], bu[2];
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int i = 2 * t + c;
-                        const double lb = sh.lb[i], ub = sh.ub[i];
-                        if (polish) {
-                            const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
-                            const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
-                            db[c] = dbu + dbl;
-                            bu[c] = -BX(F_Q, sg, c) + dbu * ub + dbl * lb;
-                        } else if (boxed) {
-                            const double rpu = BX(F_U, sg, c) + BX(F_SU, sg, c) - ub;
-                            const double rpl = -BX(F_U, sg, c) + BX(F_SL, sg, c) + lb;
-                            db[c] = BX(F_ZU, sg, c) * frcp(BX(F_SU, sg, c)) + BX(F_ZL, sg, c) * frcp(BX(F_SL, sg, c));
-                            bu[c] = -BX(F_RD, sg, c) + (BX(F_SU, sg, c) * BX(F_ZU, sg, c) - BX(F_ZU, sg, c) * rpu) * frcp(BX(F_SU, sg, c)) -
-                                    (BX(F_SL, sg, c) * BX(F_ZL, sg, c) - BX(F_ZL, sg, c) * rpl) * frcp(BX(F_SL, sg, c));
-                        } else {
-                            db[c] = 0.0;
-                            bu[c] = -BX(F_RD, sg, c);
-                        }
-                    }
-                    if (own[sg]) {
-#pragma unroll
-                        for (int e = 0; e < 5; ++e)
-                            wr2(r + 2 * e, isN[sg] ? wn[2 * e] : Wa[sg][2 * e], isN[sg] ? wn[2 * e + 1] : Wa[sg][2 * e + 1]);
-                        wr2(r + O_BU, bu[0], bu[1]);
-                        wr2(r + O_DB, db[0], db[1]);
-                    }
-                }
-                RT_MARK(4);
-                if constexpr (HET) factor_and_back();
-            }
-            if constexpr (!HET) factor_mm();
-            RT_MARK(5);
-            // ================= solves =================
-            // fully unrolled: k is a constant in every branch below (precise register lifetimes)
-            // the refinement solve (k = 2 of a normal trip) only once mu <= REFINE_MU; before
-            // that its correction is zero
-            const bool refine = mu <= REFINE_MU;
-            double ra[RS];   // polish: multiplier estimates of the active rows (set at k = 0, live only in a polish trip)
-#pragma unroll
-            for (int k = 0; k < POLISH_REFINE + 1; ++k) {
-                if (k == 3 && !any_polish) break;
-                const bool run = active && (polish || k < 3);
-                const bool solve = run && (polish || k != 2 || refine);
-                if constexpr (HET) {
-                    if (k > 0 && solve) back_linear();
-                    RT_MARK(6);
-                    if (solve) forward();
-                } else {
-                    // the matrix-core passes run for the whole wave; groups that sit out only skip the stores
-                    if (__any(solve)) {
-                        if (k > 0) back_mm();
-                        RT_MARK(6);
-                        forward_mm();
-                    }
-                }
-                RT_MARK(7);
-                if (!run) continue;
-                double dy[2][4], dv[2][2];
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg) {
-                    if (solve) {
-                        rd4((kseg[sg] - 1) * REC + O_BX, dy[sg]);
-                        rd2((kseg[sg] - 1) * REC + O_BU, dv[sg][0], dv[sg][1]);
-                    } else {
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) dy[sg][a] = 0.0;
-                        dv[sg][0] = dv[sg][1] = 0.0;
-                    }
-                }
-                wb();
-                if (polish) {
-                    // update: yg += d (G dx - ryg); yu += dbu (dx - ryu); yl += dbl (-dx - ryl); x += dx
-                    FOR_SLOTS_BEGIN
-                        const double d = act(s) ? idl : 0.0;
-                        // ryg of this solve: w - G x at the x before the update (x = 0 at k = 0)
-                        const double ryg = d != 0.0 ? in.w - (k == 0 ? 0.0 : dot4(c, xvv[sg])) : 0.0;
-                        ra[s] = fma(d, dot4(c, dy[sg]) - ryg, k == 0 ? 0.0 : ra[s]);
-                    FOR_SLOTS_END
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) {
-                        const int t = kseg[sg] - 1;
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            const int i = 2 * t + c;
-                            const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
-                            const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
-                            const double x_old = k == 0 ? 0.0 : BX(F_VX, sg, c);
-                            const double ryu = dbu != 0.0 ? sh.ub[i] - x_old : 0.0;
-                            const double ryl = dbl != 0.0 ? -sh.lb[i] + x_old : 0.0;
-                            BX(F_E1, sg, c) = fma(dbu, dv[sg][c] - ryu, k == 0 ? 0.0 : BX(F_E1, sg, c));
-                            BX(F_E2, sg, c) = fma(dbl, -dv[sg][c] - ryl, k == 0 ? 0.0 : BX(F_E2, sg, c));
-                            BX(F_VX, sg, c) = own[sg] ? x_old + dv[sg][c] : 0.0;
-                        }
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) xvv[sg][a] = (k == 0 ? 0.0 : xvv[sg][a]) + dy[sg][a];
-                    }
-                    if (k < POLISH_REFINE) {
-                        // next right-hand side of the refinement
-                        double acc[2][4];
-#pragma unroll
-                        for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) acc[sg][a] = -0.0;
-                        FOR_SLOTS_BEGIN
-                            const double d = act(s) ? idl : 0.0;
-                            const double gx = dot4(c, xvv[sg]);
-                            const double ryg = d != 0.0 ? in.w - gx : 0.0;
-                            const double t = -(ra[s] - d * ryg);
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) acc[sg][a] = fma(t, c[a], acc[sg][a]);
-                        FOR_SLOTS_END
-                        wb();
-                        write_bx(acc, xvv, -1.0);
-#pragma unroll
-                        for (int sg = 0; sg < 2; ++sg) {
-                            const int t = kseg[sg] - 1;
-                            double bu[2];
-#pragma unroll
-                            for (int c = 0; c < 2; ++c) {
-                                const int i = 2 * t + c;
-                                const double dbu = (boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c)) ? idl : 0.0;
-                                const double dbl = (boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c)) ? idl : 0.0;
-                                const double ryu = dbu != 0.0 ? sh.ub[i] - BX(F_VX, sg, c) : 0.0;
-                                const double ryl = dbl != 0.0 ? -sh.lb[i] + BX(F_VX, sg, c) : 0.0;
-                                const double rx = M.Rmul(c, BX(F_VX, sg, 0), BX(F_VX, sg, 1));
-                                bu[c] = -BX(F_Q, sg, c) - rx - BX(F_E1, sg, c) + BX(F_E2, sg, c) + dbu * ryu - dbl * ryl;
-                            }
-                            if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
-                        }
-                    } else {
-                        // verification (oracle/qp.py::polish_step acceptance test)
-                        double viol = -INFINITY, wsc = 0.0, ysc = 0.0, ymin = 0.0;
-                        bool fin = true;
-#pragma unroll
-                        for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                            for (int c = 0; c < 2; ++c) {
-                                const int i = 2 * (kseg[sg] - 1) + c;
-                                if (own[sg]) {
-                                    if (boxed) {
-                                        viol = fmax(viol, fmax(BX(F_VX, sg, c) - sh.ub[i], sh.lb[i] - BX(F_VX, sg, c)));
-                                        wsc = fmax(wsc, fmax(fabs(sh.lb[i]), fabs(sh.ub[i])));
-                                    }
-                                    ysc = fmax(ysc, fmax(fabs(BX(F_E1, sg, c)), fabs(BX(F_E2, sg, c))));
-                                    ymin = fmin(ymin, fmin(BX(F_E1, sg, c), BX(F_E2, sg, c)));
-                                    fin = fin && isfinite(BX(F_VX, sg, c));
-                                }
-                            }
-                        bool paired[RS];
-#pragma unroll
-                        for (int s = 0; s < RS; ++s) paired[s] = false;
-                        if (P.r_partner) {
-#pragma unroll
-                            for (int s = 0; s < RS; ++s)
-                                scr[s][lane] = act(s) ? ra[s] : NAN;
-                            wb();
-#pragma unroll
-                            for (int s = 0; s < RS; ++s) {
-                                const int pr = sh.partner[s * G16 + j];   // -1 in unused slots
-                                paired[s] = pr >= 0 && act(s) &&
-                                            !isnan(scr[pr / G16][(lane & 48) + (pr % G16)]);
-                            }
-                            wb();
-                        }
-#pragma unroll
-                        for (int s = 0; s < RS; ++s) {
-                            const int sg = s / RSEG;
-                            if (valid(s)) {
-                                double c[4];
-                                cf(s, c);
-                                const double w = wv.w[s][lane];
-                                viol = fmax(viol, dot4(c, xvv[sg]) - w);
-                                wsc = fmax(wsc, fabs(w));
-                                ysc = fmax(ysc, fabs(ra[s]));
-                                ymin = paired[s] ? ymin : fmin(ymin, ra[s]);
-                            }
-                        }
-                        viol = row_max(viol);
-                        wsc = row_max(wsc);
-                        ysc = row_max(ysc);
-                        ymin = row_min(ymin);
-                        const double finv = row_min(fin ? 1.0 : 0.0);
-                        if (finv > 0.0 && viol <= POLISH_TOL * (1.0 + wsc) && ymin >= -POLISH_TOL * (1.0 + ysc)) {
-#pragma unroll
-                            for (int sg = 0; sg < 2; ++sg)
-                                if (own[sg]) {
-                                    BX(F_U, sg, 0) = BX(F_VX, sg, 0);
-                                    BX(F_U, sg, 1) = BX(F_VX, sg, 1);
-                                }
-                            finish(CARMPC_OPTIMAL, false);
-                            active = false;
-                        } else if constexpr (MODE == 2) {
-                            // rejected: the single-kernel launch solves the instance again from the start
-                            if (j == 0) {
-                                const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 3, 1u);
-                                W.retry_idx[seg0 + pos] = (int32_t)inst;
-                            }
-                            finish(0, false, false);
-                            active = false;
-                        }
-                        polish_failed = true;
-                    }
-                    RT_MARK(11);
-                    continue;
-                }
-                // ---------------- normal trip ----------------
-                // slot directions are rebuilt from the stage states of each solve (nothing per
-                // slot survives a pass): ds = -rp - c.dy, dz = (-rc - z ds)/s with rc = s z for the
-                // predictor and rc = s z + dsA dzA - smu for the corrector (dsA, dzA from dyA).
-                if (k == 0) {
-                    double amax = INFINITY, mua = -0.0;
-                    double dsv[RS], dzv[RS];
-                    FOR_SLOTS_BEGIN
-                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
-                        dsv[s] = -rp - dot4(c, dy[sg]);
-                        dzv[s] = (-s_[s] * z_[s] - z_[s] * dsv[s]) * frcp(s_[s]);
-                        amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
-                    FOR_SLOTS_END
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            const int i = 2 * (kseg[sg] - 1) + c;
-                            if (own[sg] && boxed) {
-                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
-                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
-                                const double rpu = uu + su - sh.ub[i];
-                                const double rpl = -uu + sl + sh.lb[i];
-                                const double dsu = -rpu - dv[sg][c], dsl = -rpl + dv[sg][c];
-                                const double dzu = (-su * zu - zu * dsu) * frcp(su);
-                                const double dzl = (-sl * zl - zl * dsl) * frcp(sl);
-                                amax = fmin(amax, fmin(fmin(ratio(su, dsu), ratio(zu, dzu)), fmin(ratio(sl, dsl), ratio(zl, dzl))));
-                                // parked in the input's state row (fields that are free until k = 1) across the reduction
-                                BX(F_E1, sg, c) = dsu;
-                                BX(F_E2, sg, c) = dzu;
-                                BX(F_E3, sg, c) = dsl;
-                                BX(F_E4, sg, c) = dzl;
-                            }
-                        }
-                    const double a = fmin(1.0, row_min(amax));
-                    for_used([&](const int s) __attribute__((always_inline)) {
-                        mua = fma(fma(a, dsv[s], s_[s]), fma(a, dzv[s], z_[s]), mua);
-                    });
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int c = 0; c < 2; ++c)
-                            if (own[sg] && boxed) {
-                                const double dsu = BX(F_E1, sg, c), dzu = BX(F_E2, sg, c);
-                                const double dsl = BX(F_E3, sg, c), dzl = BX(F_E4, sg, c);
-                                mua = fma(fma(a, dsu, BX(F_SU, sg, c)), fma(a, dzu, BX(F_ZU, sg, c)), mua);
-                                mua = fma(fma(a, dsl, BX(F_SL, sg, c)), fma(a, dzl, BX(F_ZL, sg, c)), mua);
-                                BX(F_E1, sg, c) = dsu * dzu;   // predictor products, kept for k = 1
-                                BX(F_E2, sg, c) = dsl * dzl;
-                            }
-                    const double sg3 = row_sum(mua) * inv_m / mu;
-                    smu = sg3 * sg3 * sg3 * mu;
-                    double acc[2][4];
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
-                    FOR_SLOTS_BEGIN
-                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
-                        const double rc = s_[s] * z_[s] + dsv[s] * dzv[s] - smu;
-                        const double t = (rc - z_[s] * rp) * frcp(s_[s]);   // unused slot: finite, times c = 0
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(t, c[aa], acc[sg][aa]);
-                    FOR_SLOTS_END
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) dyA[sg][aa] = dy[sg][aa];
-                    double zero4[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-                    wb();
-                    write_bx(acc, zero4, 0.0);
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) {
-                        const int t = kseg[sg] - 1;
-                        double bu[2];
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            const int i = 2 * t + c;
-                            if (boxed) {
-                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
-                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
-                                const double rpu = uu + su - sh.ub[i];
-                                const double rpl = -uu + sl + sh.lb[i];
-                                const double rcu = su * zu + BX(F_E1, sg, c) - smu;
-                                const double rcl = sl * zl + BX(F_E2, sg, c) - smu;
-                                bu[c] = -BX(F_RD, sg, c) + (rcu - zu * rpu) * frcp(su) - (rcl - zl * rpl) * frcp(sl);
-                            } else {
-                                bu[c] = -BX(F_RD, sg, c);
-                            }
-                        }
-                        if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
-                    }
-                    RT_MARK(8);
-                } else if (k == 1) {
-                    // corrector direction; refinement right-hand side -(H du + G'dz + rd + box)
-                    double acc[2][4];
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = -0.0;
-                    if (refine)
-                    FOR_SLOTS_BEGIN
-                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
-                        const double dsa = -rp - dot4(c, dyA[sg]);
-                        const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
-                        const double rc = s_[s] * z_[s] + dsa * dza - smu;
-                        const double ds = -rp - dot4(c, dy[sg]);
-                        const double dz = (-rc - z_[s] * ds) * frcp(s_[s]);   // unused slot: smu, times c = 0
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) acc[sg][aa] = fma(-dz, c[aa], acc[sg][aa]);
-                    FOR_SLOTS_END
-                    wb();
-                    if (refine) write_bx(acc, dy, -1.0);
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) {
-                        const int t = kseg[sg] - 1;
-                        double bu[2];
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            const int i = 2 * t + c;
-                            double dzu = 0.0, dzl = 0.0;
-                            if (own[sg] && boxed) {
-                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
-                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c), uu = BX(F_U, sg, c);
-                                const double rpu = uu + su - sh.ub[i];
-                                const double rpl = -uu + sl + sh.lb[i];
-                                const double rcu = su * zu + BX(F_E1, sg, c) - smu;
-                                const double rcl = sl * zl + BX(F_E2, sg, c) - smu;
-                                const double dsu = -rpu - dv[sg][c], dsl = -rpl + dv[sg][c];
-                                dzu = (-rcu - zu * dsu) * frcp(su);
-                                dzl = (-rcl - zl * dsl) * frcp(sl);
-                                BX(F_E1, sg, c) = dsu;
-                                BX(F_E2, sg, c) = dzu;
-                                BX(F_E3, sg, c) = dsl;
-                                BX(F_E4, sg, c) = dzl;
-                            }
-                            const double rdu = M.Rmul(c, dv[sg][0], dv[sg][1]);
-                            bu[c] = -(rdu + BX(F_RD, sg, c) + (dzu - dzl));
-                        }
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) BX(F_VX, sg, c) = dv[sg][c];
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) xvv[sg][aa] = dy[sg][aa];
-                        if (own[sg]) wr2(t * REC + O_BU, bu[0], bu[1]);
-                    }
-                    RT_MARK(9);
-                } else if (k == 2) {
-                    // corrected direction (dy_T = corrector + correction), step length, update
-                    double dyT[2][4];
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) dyT[sg][aa] = xvv[sg][aa] + dy[sg][aa];
-                    double amax = INFINITY, dsv[RS], dzv[RS];
-                    FOR_SLOTS_BEGIN
-                        const double rp = dot4(c, xs[sg]) + s_[s] - in.w;
-                        const double dsa = -rp - dot4(c, dyA[sg]);
-                        const double dza = (-s_[s] * z_[s] - z_[s] * dsa) * frcp(s_[s]);
-                        // the centering term belongs to rows with a multiplier (z > 0 on every used
-                        // slot, z = 0 on unused ones, which must keep dz = 0)
-                        const double rc = s_[s] * z_[s] + dsa * dza - (z_[s] > 0.0 ? smu : 0.0);
-                        dsv[s] = -rp - dot4(c, dyT[sg]);
-                        dzv[s] = (-rc - z_[s] * dsv[s]) * frcp(s_[s]);
-                        amax = fmin(amax, fmin(ratio(s_[s], dsv[s]), ratio(z_[s], dzv[s])));
-                    FOR_SLOTS_END
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            BX(F_VX, sg, c) += dv[sg][c];
-                            if (own[sg] && boxed) {
-                                const double cu = dv[sg][c];
-                                const double su = BX(F_SU, sg, c), sl = BX(F_SL, sg, c);
-                                const double zu = BX(F_ZU, sg, c), zl = BX(F_ZL, sg, c);
-                                const double e1 = BX(F_E1, sg, c) - cu;
-                                const double e2 = fma(zu * cu, frcp(su), BX(F_E2, sg, c));
-                                const double e3 = BX(F_E3, sg, c) + cu;
-                                const double e4 = fma(-zl * cu, frcp(sl), BX(F_E4, sg, c));
-                                BX(F_E1, sg, c) = e1;
-                                BX(F_E2, sg, c) = e2;
-                                BX(F_E3, sg, c) = e3;
-                                BX(F_E4, sg, c) = e4;
-                                amax = fmin(amax, fmin(fmin(ratio(su, e1), ratio(zu, e2)), fmin(ratio(sl, e3), ratio(zl, e4))));
-                            }
-                        }
-                    const double a = fmin(1.0, STEP_FRAC * row_min(amax));
-                    for_used([&](const int s) __attribute__((always_inline)) {
-                        s_[s] = fma(a, dsv[s], s_[s]);
-                        z_[s] = fma(a, dzv[s], z_[s]);
-                    });
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) {
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            if (own[sg]) BX(F_U, sg, c) = fma(a, BX(F_VX, sg, c), BX(F_U, sg, c));
-                            if (own[sg] && boxed) {
-                                BX(F_SU, sg, c) = fma(a, BX(F_E1, sg, c), BX(F_SU, sg, c));
-                                BX(F_ZU, sg, c) = fma(a, BX(F_E2, sg, c), BX(F_ZU, sg, c));
-                                BX(F_SL, sg, c) = fma(a, BX(F_E3, sg, c), BX(F_SL, sg, c));
-                                BX(F_ZL, sg, c) = fma(a, BX(F_E4, sg, c), BX(F_ZL, sg, c));
-                            }
-                        }
-#pragma unroll
-                        for (int aa = 0; aa < 4; ++aa) xs[sg][aa] = fma(a, dyT[sg][aa], xs[sg][aa]);
-                    }
-                    polish_failed = false;
-                    ++it;
-                    RT_MARK(10);
-                }
-            }
-            if constexpr (!HET) {
-                // the polish's pair check borrows the record buffer of the whole wave: restore the zero slots
-                if (any_polish && P.r_partner) {
-                    wb();
-                    for (int t = j; t < N; t += G16) rec[t * REC + O_ZERO] = 0.0;
-                    wb();
-                }
+                if constexpr (MODE != 2) solve_phase(std::false_type{}, active && !polish);
             }
         }
     }
