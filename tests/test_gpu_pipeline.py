@@ -39,3 +39,29 @@ def test_pipeline_equals_single_kernel(gpu_available, env, N):
     assert ok.sum() > B // 8
     np.testing.assert_allclose(u1.cpu().numpy()[ok], u0.cpu().numpy()[ok], rtol=0, atol=1e-12)
     assert torch.equal(u1[st1 != 0], u0[st1 != 0])                           # (infeasible instances: last iterate or zeros)
+
+
+def test_pipeline_with_disturbance_and_xref_equals_chunked_single_kernel(gpu_available):
+    """Per-instance disturbance estimates and explicit references through the pipeline (65,536
+    instances in one call) against the same instances solved in chunks below the pipeline's
+    size threshold (single kernel)."""
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    qp = QPProblem(N=20, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    qp.set_disturbance(np.array([0.0, 0.0, 0.02, 0.05]))
+    B, chunk = 65536, 16384
+    rng = np.random.default_rng(5)
+    X = torch.as_tensor(_x0(rng, asm.goal[0], B)).to(qp.device)
+    D = torch.as_tensor(rng.uniform(-0.5, 0.5, B)).to(qp.device)
+    R = torch.as_tensor(np.tile(asm.goal, (B, 1)) + rng.normal(scale=0.05, size=(B, 4))).to(qp.device)
+    u1, st1, it1 = qp.solve(X, xref=R, dist=D)
+    parts = [qp.solve(X[i:i + chunk], xref=R[i:i + chunk], dist=D[i:i + chunk]) for i in range(0, B, chunk)]
+    torch.cuda.synchronize()
+    u0 = torch.cat([p[0] for p in parts]); st0 = torch.cat([p[1] for p in parts]); it0 = torch.cat([p[2] for p in parts])
+    assert torch.equal(st1, st0) and torch.equal(it1, it0)
+    assert int((st0 == 0).sum()) > B // 8
+    assert torch.equal(u1, u0)
