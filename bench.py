@@ -121,7 +121,7 @@ def oracle_sample(envs, N, X, offsets, sample: int, threads: int, xref=None):
         res["t_all"] += time.perf_counter() - t0
         res["n"] += len(sel)
         res["iters"][name] = float(it.mean())
-        one = sel[:max(64, len(sel) // 16)]
+        one = sel[:max(64, len(sel) // 8)]
         t0 = time.perf_counter()
         cp.solve(X[one], xr[:len(one)] if xr is not None else None, threads=1)
         res["t_one"] += time.perf_counter() - t0
@@ -458,7 +458,8 @@ def parse_args(argv=None):
     ap.add_argument("--per-gpu", type=int, default=0, help="instances per rank (default: the configuration's batch)")
     ap.add_argument("--backend", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--cpu-threads", type=int, default=0, help="--backend cpu: threads per rank (0 = all)")
-    ap.add_argument("--cpu-sample", type=int, default=24576)
+    ap.add_argument("--cpu-sample", type=int, default=131072,
+                    help="instances of rank 0's shard timed on the host (all cores; an eighth of them on one thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--per-problem-launches", action="store_true",
                     help="one carmpc_solve_batch launch per environment instead of one carmpc_solve_segments call")
