@@ -1,23 +1,26 @@
 // ipm_riccati.hip -- grouped stage-form Mehrotra IPM: 16 lanes per QP, 4 QPs per wavefront.
 //
 // Replaces the per-step cvxpy solve of lib/mpc.py:334-335 / 477-478 with a Mehrotra
-// predictor-corrector IPM (restated on the CPU in oracle/qp.py::ipm), applying M^{-1} by a backward Riccati recursion and a
-// forward roll-out over the horizon (oracle/riccati.py, the CPU restatement this kernel
-// follows line by line).  Every QP row acts on one predicted state x_k (mpc.py:196-253),
+// predictor-corrector IPM (restated on the CPU in oracle/qp.py::ipm), applying M^{-1} by a backward
+// Riccati recursion and a forward roll-out over the horizon (oracle/riccati.py, the CPU restatement
+// this kernel follows line by line).  Every QP row acts on one predicted state x_k (mpc.py:196-253),
 // and H = R_hat + S'Q_hat S (matrix_gen.py:35-72), so
 //     M = H + G'DG + diag(box) = R_hat + diag(Db) + sum_k S_k'(Qbar_k + W_k) S_k.
 //
 // Layout (one QP per 16-lane DPP row; group g = lane>>4, j = lane&15):
 //   * row state in registers: lane j owns stage j+1 (segment 0) and j+17 (segment 1) -- the
 //     rows of those stages sit in its 2 x 8 slots; stage-N rows that do not fit the owner
-//     spill into the segments whose stage number exceeds N (capi.hip::riccati_layout);
-//     the owner of stage t+1 also owns the input u_t (both components) and its box rows;
-//   * stage recursions (adjoints, Riccati factorization, backward/forward solves) run
-//     redundantly in all 16 lanes of the group -- scalar code, no cross-lane traffic --
-//     reading/writing per-stage records in LDS (W_k, rhs, factor K_t / Re_t, y_k, v_t);
+//     go to the segments whose stage number exceeds N (capi.hip::riccati_layout);
+//     the owner of stage t+1 also owns the input u_t (both components) and its box rows (LDS);
+//   * stage recursions (adjoints, Riccati factorization, backward/forward solves) exchange
+//     per-stage records in LDS (W_k, rhs, factor K_t / Re_t, y_k, v_t) with the row phases.
+//     Shared-model problems run them on the matrix cores, one 4x4 matrix entry per lane (see
+//     "stage recursions on the matrix cores" below); per-instance models (HET) run them as scalar
+//     code repeated in the 16 lanes of the group;
 //   * per-QP reductions are 16-lane DPP butterflies (lanes.h), bitwise row-uniform.
-// The 4 groups of a wave advance trip by trip together; a finished group idles until the
-// wave's 4 instances are done.
+// The 4 groups of a wave advance trip by trip together (one trip = one IPM iteration or one
+// polish); a group that finishes an instance claims its next one from an atomic counter at once.
+// Large solves run as three launches of this kernel (MODE, launch pipeline at the end of the file).
 #include "carmpc_internal.h"
 #include "lanes.h"
 
@@ -54,17 +57,17 @@ __device__ unsigned long long carmpc_ric_cycles[12];
 #define RT_FLUSH() do {} while (0)
 #endif
 
-// Unroll factor of the software-pipelined stage loops (forward, backward, roll-out,
-// factorization; adjoint pass): > 1 lets the compiler rename the one-stage-ahead prefetch
-// registers instead of copying them every stage.  Bench (1 GPU, QP/s) for unroll 1 / 2 / 4 /
-// 5 / 10 of both: 7.05M / 7.52M / 7.73M / 7.80M / 7.76M (tools/gpu/sched_sweep.sh variants).
+// Unroll factor of the scalar stage loops (per-instance models and the initial roll-out; forward,
+// backward, factorization, adjoint): > 1 lets the compiler rename the one-stage-ahead prefetch
+// registers instead of copying them every stage.  Measured when the shared-model kernels still ran
+// these loops (1 GPU, QP/s) for unroll 1 / 2 / 4 / 5 / 10: 7.05M / 7.52M / 7.73M / 7.80M / 7.76M.
 #ifndef CARMPC_RIC_UNROLL
 #define CARMPC_RIC_UNROLL 5
 #endif
 #ifndef CARMPC_RIC_UNROLL_ADJ
 #define CARMPC_RIC_UNROLL_ADJ 5
 #endif
-// Stage records: all 16 lanes of a group hold bitwise-identical values (redundant scalar
+// Scalar stage loops: all 16 lanes of a group hold bitwise-identical values (redundant
 // recursions), and every lane stores them (same address, same bits) -- no exec-mask branch
 // per stage.  Lane-0-only stores (CARMPC_RIC_LANE0_WRITE) measured 7.81M vs 8.05M QP/s.
 #ifdef CARMPC_RIC_LANE0_WRITE
