@@ -137,17 +137,22 @@ int carmpc_problem_get(const carmpc_problem* prob, double* T, double* S, double*
  *   x0    B*nx  device, absolute state (constraints use it as is, mpc.py:319)
  *   xref  B*nx  device or NULL (NULL = goal; cost uses x0 - xref, mpc.py:320)
  *   u_out B*n   device, optimal input sequence u_0..u_{N-1}
- *   status, iters  B int32 device (iters may be NULL)                          */
+ *   status, iters  B int32 device (iters may be NULL)
+ * Stream-ordered on `stream`.  Device memory beyond the arguments comes from the stream-ordered
+ * allocator: a claim counter, and for large batches of the grouped kernel (which then runs as
+ * an iteration launch, a polish launch and a launch for the instances whose polish was rejected)
+ * the work lists between those launches, 76 bytes per instance.  Results do not depend on which
+ * form ran. */
 int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
                        double* u_out, int32_t* status, int32_t* iters,
                        const carmpc_settings* settings, hipStream_t stream);
 
 /* carmpc_solve_batch for callers that cannot allocate: code under HIP graph capture, tight
  * serving loops, harnesses that forbid hipMalloc.  It has no counterpart in the reference.  Same
- * arguments, results and kernels as carmpc_solve_batch; the kernels' claim counter (the only
- * device memory the solve uses beyond its inputs and outputs) lives in a 256-byte static device
- * array of the library instead of a stream-ordered allocation, and the call makes no hipMalloc,
- * hipFree or other allocating call.  batch <= CARMPC_NOALLOC_MAX_BATCH, else CARMPC_EUNSUPPORTED.
+ * arguments and results as carmpc_solve_batch; it always runs the single-launch form of the
+ * kernels, whose claim counter (the only device memory that form uses beyond its inputs and
+ * outputs) lives in a 256-byte static device array of the library instead of a stream-ordered
+ * allocation, and the call makes no hipMalloc, hipFree or other allocating call.  batch <= CARMPC_NOALLOC_MAX_BATCH, else CARMPC_EUNSUPPORTED.
  * All calls on one GPU share that array: the counter is cleared at the start of each call (on
  * `stream`), and two calls whose kernels overlap on one GPU -- from different streams or threads --
  * race on it.  Call it with the problem's device current. */
