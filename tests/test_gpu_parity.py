@@ -187,6 +187,37 @@ def test_flags_and_edge_cases(gpu_available):
     assert torch.equal(u, u2) and torch.equal(st, st2)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_non_finite_x0(gpu_available, kernel):
+    """NaN / infinite measurements end with a status (numerical or infeasible, as the oracle reports them),
+    never with `optimal`, and do not disturb their neighbours -- in the single launch (small batch) and in
+    the three-launch form of the grouped kernel (large batch)."""
+    import torch
+    from oracle.cpu import CpuProblem
+    for name in ("RoadEnv", "RoadMultipleCarsEnv"):
+        asm, qp = _setup(name, 20)
+        rng = np.random.default_rng(3)
+        for B in ((32, 65536) if kernel == 7 else (32,)):
+            X = _random_x0(rng, asm.goal[0], B)
+            bad = [3, 7, 11, 13, 17]
+            Xp = X.copy()
+            Xp[3, :] = np.nan
+            Xp[7, 2] = np.inf
+            Xp[11, 0] = -np.inf
+            Xp[13, 1] = np.nan
+            Xp[17, 3] = 1e300
+            u0, st0, _ = qp.solve(torch.as_tensor(X).cuda(), settings=_settings(kernel))
+            u1, st1, _ = qp.solve(torch.as_tensor(Xp).cuda(), settings=_settings(kernel))
+            st1 = st1.cpu().numpy()
+            _, sc, _ = CpuProblem(asm).solve(Xp[:32])
+            np.testing.assert_array_equal(st1[bad], sc[bad], err_msg=f"{name} B={B}")
+            assert set(st1[bad]) <= {1, 3}
+            keep = np.ones(B, bool)
+            keep[bad] = False
+            assert np.array_equal(st1[keep], st0.cpu().numpy()[keep])
+            assert torch.equal(u1[torch.as_tensor(keep)], u0[torch.as_tensor(keep)])
+
+
 def test_terminal_fallback_and_short_horizon(gpu_available, tmp_path):
     """Missing terminal-set file -> goal box (mpc.py:107-117); N=5 exercises kernel padding (n=10 -> 16)."""
     import torch
