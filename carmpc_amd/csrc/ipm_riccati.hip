@@ -952,6 +952,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     double bnorm = 1.0, qnorm = 1.0;
     int it = 0, npol = 0;   // iterations; polish points passed over (pipeline rounds > 0)
     bool polish_failed = false;
+    // Polish correction (shared-model kernels): when the acceptance test rejects the first attempt at a polish
+    // point and names rows to drop (active, negative multiplier) or to add (inactive, violated), the group's
+    // next trip polishes again on that corrected set (act_next: the set, bit 31 = such a trip is due); a second
+    // rejection stands.
+    unsigned act_next = 0;
     // write the result of the current instance and move the group to its next one
     auto finish = [&](int st, bool zero_u, bool write = true) {
         if (write) {
@@ -1023,6 +1028,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             it = 0;
             npol = 0;
             polish_failed = false;
+            if constexpr (!HET) act_next = 0;
             if (row_max(bad) > 0.0) {
                 finish(CARMPC_PRIMAL_INFEASIBLE, true);
                 active = false;
@@ -1102,8 +1108,23 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             bool polish = false;
             // polish: the active set (rows with s < z) as a bit per slot, fixed when the polish factorizes;
             // the polish loops test it instead of reading s and z (which they leave alone)
+            // (shared-model kernels: bits 16.. hold the box rows of the lane's inputs, upper and lower bound of
+            // input (sg, c) at 16 + 4 sg + 2 c and the bit above; per-instance kernels compare slack and multiplier)
             unsigned actm = 0;
+#define RIC_REPOL (!HET && (act_next >> 31) != 0)   // this trip is the second attempt of a polish
+            if constexpr (!HET) {
+                if (RIC_REPOL) actm = act_next & 0xFFFFFFu;
+            }
             auto act = [&](int s) { return ((actm >> s) & 1u) != 0; };
+            auto box_bit = [](int sg, int c, int lower) { return 16 + (sg * 2 + c) * 2 + lower; };
+            auto act_ub = [&](int sg, int c) {
+                if constexpr (HET) return boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c);
+                else return ((actm >> box_bit(sg, c, 0)) & 1u) != 0;
+            };
+            auto act_lb = [&](int sg, int c) {
+                if constexpr (HET) return boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c);
+                else return ((actm >> box_bit(sg, c, 1)) & 1u) != 0;
+            };
             if (MODE != 2 && active) {
                 double lz[2][4], musum = -0.0;
 #pragma unroll
@@ -1293,8 +1314,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 #pragma unroll
                             for (int c = 0; c < 2; ++c)
                                 if (own[sg] && boxed) {
-                                    m |= (BX(F_SU, sg, c) < BX(F_ZU, sg, c) ? 1u : 0u) << (16 + (sg * 2 + c) * 2);
-                                    m |= (BX(F_SL, sg, c) < BX(F_ZL, sg, c) ? 1u : 0u) << (17 + (sg * 2 + c) * 2);
+                                    m |= (BX(F_SU, sg, c) < BX(F_ZU, sg, c) ? 1u : 0u) << box_bit(sg, c, 0);
+                                    m |= (BX(F_SL, sg, c) < BX(F_ZL, sg, c) ? 1u : 0u) << box_bit(sg, c, 1);
                                 }
                         W.pend_mask[(seg0 + inst) * G16 + j] = m;
                         if (j == 0) {
@@ -1312,21 +1333,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             if constexpr (MODE == 2) {
                 // the hand-off record replaces residuals and decisions
                 polish = true;
-                if (active) {
-                    const unsigned m = W.pend_mask[(seg0 + inst) * G16 + j];
-                    actm = m & 0xFFFFu;
+                if (active && !RIC_REPOL) {
+                    actm = W.pend_mask[(seg0 + inst) * G16 + j];
                     it = W.pend_it[seg0 + inst];
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            // the polish only compares slack with multiplier: restore the outcome of the comparison
-                            const bool bu = (m >> (16 + (sg * 2 + c) * 2)) & 1u, bl = (m >> (17 + (sg * 2 + c) * 2)) & 1u;
-                            BX(F_SU, sg, c) = bu ? 0.0 : 1.0;
-                            BX(F_ZU, sg, c) = bu ? 1.0 : 0.0;
-                            BX(F_SL, sg, c) = bl ? 0.0 : 1.0;
-                            BX(F_ZL, sg, c) = bl ? 1.0 : 0.0;
-                        }
                 }
             }
             const bool any_polish = __any(polish);
@@ -1367,6 +1376,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     }
     RT_FLUSH();
     }   // segments
+#undef RIC_REPOL
 }
 
 }  // namespace
