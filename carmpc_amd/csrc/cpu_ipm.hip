@@ -43,6 +43,7 @@ namespace {
 
 constexpr double kPolishMu = 1e-6, kPolishDelta = 1e-10, kPolishTol = 1e-11;
 constexpr int kPolishRefine = 3;
+constexpr int kPolishCorrections = 1;   // correction rounds of a rejected polish
 constexpr double kInf = std::numeric_limits<double>::infinity();
 
 inline void mat4(const double* X, const double* Y, double* Z) {   // Z = X Y
@@ -284,6 +285,9 @@ struct Solver {
 
     // Active-set polish: equality-constrained KKT on the rows with s < z, by iterative refinement
     // on the regularised factor (d = 1/delta on active rows).  Returns true when x is accepted.
+    // A rejected attempt names what is wrong with its active set -- active rows whose multiplier
+    // fails the sign test, inactive rows that are violated; the polish runs once more on the set
+    // with those rows dropped / added (kPolishCorrections, as the grouped device kernel does).
     bool polish(const double* lbv, const double* ubv) {
         const double idl = 1.0 / kPolishDelta;
         const bool boxed = P.boxed;
@@ -291,6 +295,20 @@ struct Solver {
         for (int i = 0; i < n; ++i) {
             dbu[i] = (boxed && su[i] < zu[i]) ? idl : 0.0;
             dbl[i] = (boxed && sl[i] < zl[i]) ? idl : 0.0;
+        }
+        for (int attempt = 0;; ++attempt) {
+            if (polish_attempt(lbv, ubv, attempt < kPolishCorrections)) return true;
+            if (attempt >= kPolishCorrections || !polish_changed) return false;
+        }
+    }
+
+    bool polish_changed = false;   // the last rejected attempt changed the active set
+    // one attempt on the active set in d / dbu / dbl; when `correct`, a rejection updates the set
+    bool polish_attempt(const double* lbv, const double* ubv, bool correct) {
+        const double idl = 1.0 / kPolishDelta;
+        const bool boxed = P.boxed;
+        polish_changed = false;
+        for (int i = 0; i < n; ++i) {
             dbox[i] = dbu[i] + dbl[i];
             x[i] = yu[i] = yl[i] = 0.0;
         }
@@ -343,7 +361,27 @@ struct Solver {
                 ymin = std::min(ymin, std::min(yu[i], yl[i]));
             }
         }
-        return fin && viol <= kPolishTol * (1.0 + wsc) && ymin >= -kPolishTol * (1.0 + ysc);
+        const double vtol = kPolishTol * (1.0 + wsc), ytol = -kPolishTol * (1.0 + ysc);
+        if (fin && viol <= vtol && ymin >= ytol) return true;
+        if (!fin || !correct) return false;
+        for (int r = 0; r < p; ++r) {   // (t: the next d, so that the pair test reads the old set)
+            const int pr = P.partner[r];
+            const bool paired = d[r] > 0.0 && pr >= 0 && d[pr] > 0.0;
+            if (d[r] > 0.0) t[r] = (!paired && yg[r] < ytol) ? 0.0 : idl;
+            else t[r] = gu[r] - w[r] > vtol ? idl : 0.0;
+        }
+        for (int r = 0; r < p; ++r) {
+            polish_changed = polish_changed || t[r] != d[r];
+            d[r] = t[r];
+        }
+        for (int i = 0; i < n && boxed; ++i) {
+            const double nu = dbu[i] > 0.0 ? (yu[i] < ytol ? 0.0 : idl) : (x[i] - ubv[i] > vtol ? idl : 0.0);
+            const double nl = dbl[i] > 0.0 ? (yl[i] < ytol ? 0.0 : idl) : (lbv[i] - x[i] > vtol ? idl : 0.0);
+            polish_changed = polish_changed || nu != dbu[i] || nl != dbl[i];
+            dbu[i] = nu;
+            dbl[i] = nl;
+        }
+        return false;
     }
 
     // QP(x0): returns the status, writes n inputs and the iteration count

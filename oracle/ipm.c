@@ -107,6 +107,10 @@ static void gtmul(const qp_t* P, const double* y, double* out) { /* out = G' y *
     }
 }
 
+/* correction rounds of a rejected polish (qp.POLISH_CORRECTIONS); 0 = the single-attempt polish */
+static int g_polish_corrections = 1;
+void oracle_set_polish_corrections(int k) { g_polish_corrections = k; }
+
 typedef struct {   /* per-thread scratch */
     double *M, *s, *z, *rp, *ds, *dz, *dsa, *dza, *t, *rc, *gv, *pv1, *pv2;
     double *su, *sl, *zu, *zl, *rpu, *rpl, *rd, *du, *dsu, *dsl, *dzu, *dzl, *dsua, *dzua, *dsla, *dzla, *nv1,
@@ -151,8 +155,11 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
     for (int i = 0; i < n; ++i) {
         dbu[i] = (boxed && W->su[i] < W->zu[i]) ? id : 0.0;
         dbl[i] = (boxed && W->sl[i] < W->zl[i]) ? id : 0.0;
-        dbox[i] = dbu[i] + dbl[i];
     }
+    /* attempt 0 on the active set of the iterate; correction rounds on the set the rejected
+     * attempt names (oracle/qp.py::polish_step) */
+    for (int attempt = 0;; ++attempt) {
+    for (int i = 0; i < n; ++i) dbox[i] = dbu[i] + dbl[i];
     factor(P, dg, dbox, W->M);   /* M is rebuilt by the IPM before its next use */
     /* first solve: rx = -q, ry = b on active rows */
     for (int r = 0; r < p; ++r) ryg[r] = dg[r] != 0.0 ? w[r] : 0.0;
@@ -205,8 +212,9 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
         const int paired = pr >= 0 && dg[r] != 0.0 && dg[pr] != 0.0;
         if (!paired && yg[r] < ymin) ymin = yg[r];
     }
+    int finite = 1;
     for (int i = 0; i < n; ++i) {
-        if (!isfinite(x[i])) return 0;
+        if (!isfinite(x[i])) finite = 0;
         if (boxed) {
             if (fabs(P->ub[i]) > wsc) wsc = fabs(P->ub[i]);
             if (fabs(P->lb[i]) > wsc) wsc = fabs(P->lb[i]);
@@ -218,7 +226,30 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
         if (yu[i] < ymin) ymin = yu[i];
         if (yl[i] < ymin) ymin = yl[i];
     }
-    return viol <= POLISH_TOL * (1.0 + wsc) && ymin >= -POLISH_TOL * (1.0 + ysc);
+    if (!finite) return 0;
+    const double vtol = POLISH_TOL * (1.0 + wsc), ytol = -POLISH_TOL * (1.0 + ysc);
+    if (viol <= vtol && ymin >= ytol) return 1;
+    if (attempt >= g_polish_corrections) return 0;
+    /* drop active rows that fail the sign test, add inactive rows that are violated */
+    int changed = 0;
+    for (int r = 0; r < p; ++r) {
+        const int pr = P->partner ? P->partner[r] : -1;
+        const int paired = pr >= 0 && dg[r] != 0.0 && dg[pr] != 0.0;
+        if (dg[r] != 0.0) W->pryg[r] = (!paired && yg[r] < ytol) ? 0.0 : id;   /* pryg: next dg (ryg is rebuilt) */
+        else W->pryg[r] = gx[r] - w[r] > vtol ? id : 0.0;
+    }
+    for (int r = 0; r < p; ++r) {
+        if (W->pryg[r] != dg[r]) changed = 1;
+        dg[r] = W->pryg[r];
+    }
+    for (int i = 0; i < n && boxed; ++i) {
+        const double nu = dbu[i] != 0.0 ? (yu[i] < ytol ? 0.0 : id) : (x[i] - P->ub[i] > vtol ? id : 0.0);
+        const double nl = dbl[i] != 0.0 ? (yl[i] < ytol ? 0.0 : id) : (P->lb[i] - x[i] > vtol ? id : 0.0);
+        if (nu != dbu[i] || nl != dbl[i]) changed = 1;
+        dbu[i] = nu; dbl[i] = nl;
+    }
+    if (!changed) return 0;
+    }
 }
 
 static int solve_one(const qp_t* P, const double* q, const double* w, double* u, work_t* W, double tol,

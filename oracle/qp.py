@@ -37,6 +37,7 @@ POLISH_MU = 1e-6           # attempt the active-set polish once mu <= POLISH_MU 
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 3          # iterative-refinement passes of the polish
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
+POLISH_CORRECTIONS = 1     # correction rounds of a rejected polish (0: the single-attempt polish of the fallback kernels)
 UNBOXED_BOUND = 1e9        # |u_i| bound assumed by the Farkas test for unboxed variables
 PRE_TOL = 1e-9             # zero-row precondition tolerance
 ZERO_ROW = 1e-12           # rows with ||G_r||_2 <= ZERO_ROW * max_r ||G_r||_2 are x0-only rows
@@ -76,7 +77,7 @@ def opposite_pairs(G, w0, E):
 
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
-        trace=None, refine=REFINE, polish=True, info=None, partner=None):
+        trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -128,7 +129,7 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
             return u, STATUS_NUMERICAL, it, z
         if polish and rpn <= tol * pscale and rdn <= tol * dscale and mu <= POLISH_MU:
             up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
-                                 partner=partner)
+                                 partner=partner, corrections=polish_corrections)
             if info is not None:
                 info.setdefault("polish", []).append((it, ok))
             if ok:
@@ -196,24 +197,50 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
 
 
 def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE,
-                partner=None):
+                partner=None, corrections=None):
     """Active-set polish.  Active set from the IPM iterate (s < z); solve the
     equality-constrained KKT [[H, A'], [A, 0]] [x; y] = [-q; b_act] by iterative refinement on
     the regularised factor  H + A'A/delta  (the IPM's M with d = 1/delta on active rows, 0 else);
     accept only if x is primal feasible and the active multipliers are nonnegative.  Rows whose
     opposite partner is also active form an equality: their multipliers can be re-split as
-    (max(y-y',0), max(y'-y,0)) without changing A'y, so they are exempt from the sign test."""
+    (max(y-y',0), max(y'-y,0)) without changing A'y, so they are exempt from the sign test.
+
+    Correction rounds (POLISH_CORRECTIONS): a rejected attempt names what is wrong with its
+    active set -- active rows whose multiplier fails the sign test, inactive rows that are
+    violated -- and the polish is repeated on the set with those rows dropped / added.  A
+    rejection with nothing to change, or of the last round, stands."""
     n = len(q)
     boxed = lb is not None
-    dg = np.where(s < z, 1.0 / delta, 0.0)
+    if corrections is None:
+        corrections = POLISH_CORRECTIONS
+    ag = s < z
+    au = su < zu if boxed else np.zeros(n, bool)
+    al = sl < zl if boxed else np.zeros(n, bool)
+    x = np.zeros(n)
+    for attempt in range(corrections + 1):
+        x, ok, fix = _polish_attempt(H, q, G, w, lb, ub, ag, au, al, delta, refine, partner)
+        if ok or fix is None or attempt == corrections:
+            return x, ok
+        nag, nau, nal = fix
+        if np.array_equal(nag, ag) and np.array_equal(nau, au) and np.array_equal(nal, al):
+            return x, False
+        ag, au, al = nag, nau, nal
+    return x, False
+
+
+def _polish_attempt(H, q, G, w, lb, ub, ag, au, al, delta, refine, partner):
+    """One polish on the active set (ag rows, au / al upper / lower bounds).  Returns x, the outcome
+    of the acceptance test and, for a rejected finite x, the corrected active set."""
+    n = len(q)
+    boxed = lb is not None
+    dg = np.where(ag, 1.0 / delta, 0.0)
     M = H + (G.T * dg) @ G
     if boxed:
-        du_ = np.where(su < zu, 1.0 / delta, 0.0); dl_ = np.where(sl < zl, 1.0 / delta, 0.0)
+        du_ = np.where(au, 1.0 / delta, 0.0); dl_ = np.where(al, 1.0 / delta, 0.0)
         M[np.diag_indices(n)] += du_ + dl_
     else:
         du_ = dl_ = np.zeros(n)
     L = _chol_guarded(M)
-    ag = dg > 0; au = du_ > 0; al = dl_ > 0
     bg = np.where(ag, w, 0.0)
     bu = np.where(au, ub, 0.0) if boxed else np.zeros(n)
     bl = np.where(al, lb, 0.0) if boxed else np.zeros(n)
@@ -236,17 +263,27 @@ def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, re
         x = x + dx; yg = yg + dyg; yu = yu + dyu; yl = yl + dyl
     wscale = 1.0 + max(np.abs(w).max() if len(w) else 0.0, np.abs(ub).max() if boxed else 0.0,
                        np.abs(lb).max() if boxed else 0.0)
-    viol = max((G @ x - w).max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
+    gxw = G @ x - w
+    viol = max(gxw.max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
                (lb - x).max() if boxed else -np.inf)
-    yg_sign = yg
+    paired = np.zeros(len(yg), bool)
     if partner is not None and len(yg):
         paired = ag & (partner >= 0) & ag[np.maximum(partner, 0)]
-        yg_sign = np.where(paired, 0.0, yg)
+    yg_sign = np.where(paired, 0.0, yg)
     ymin = min(yg_sign.min() if len(yg) else 0.0, yu.min() if boxed else 0.0, yl.min() if boxed else 0.0)
     yscale = 1.0 + max(np.abs(yg).max() if len(yg) else 0.0, np.abs(yu).max() if boxed else 0.0,
                        np.abs(yl).max() if boxed else 0.0)
-    ok = bool(viol <= POLISH_TOL * wscale and ymin >= -POLISH_TOL * yscale and np.all(np.isfinite(x)))
-    return x, ok
+    finite = bool(np.all(np.isfinite(x)))
+    vtol, ytol = POLISH_TOL * wscale, -POLISH_TOL * yscale
+    ok = bool(viol <= vtol and ymin >= ytol and finite)
+    if ok or not finite:
+        return x, ok, None
+    nag = np.where(ag, ~(~paired & (yg < ytol)), gxw > vtol)
+    nau, nal = au, al
+    if boxed:
+        nau = np.where(au, ~(yu < ytol), x - ub > vtol)
+        nal = np.where(al, ~(yl < ytol), lb - x > vtol)
+    return x, ok, (nag, nau, nal)
 
 
 def _maxstep(v, dv):

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (MAX_ITER, POLISH_DELTA, POLISH_MU, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
+from .qp import (MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -149,7 +149,7 @@ def _chol2_solve(L, b):
     return np.array([x0, x1]) if b.ndim == 1 else np.vstack([x0, x1])
 
 
-def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER):
+def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None):
     """qp.ipm + qp.polish_step in stage form for one instance.  Returns (u, status, iters)."""
     x0 = np.asarray(x0, float)
     xref = np.asarray(xref, float)
@@ -210,7 +210,7 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER):
                 if lo - w @ z > 1e-12 * (np.abs(Gtz) @ bound_abs + np.abs(w) @ z):
                     return u, STATUS_INFEASIBLE, it
         if polish:
-            x, ok = _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat)
+            x, ok = _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, polish_corrections)
             if ok:
                 return x, STATUS_OPTIMAL, it
             polish_failed = True
@@ -261,15 +261,34 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER):
         it += 1
 
 
-def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat):
-    """qp.polish_step in stage form."""
+def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=None):
+    """qp.polish_step in stage form, with its correction rounds."""
+    n = sq.n
+    if corrections is None:
+        corrections = POLISH_CORRECTIONS
+    ag = s < z
+    au = su < zu if boxed else np.zeros(n, bool)
+    al = sl < zl if boxed else np.zeros(n, bool)
+    x = np.zeros(n)
+    for attempt in range(corrections + 1):
+        x, ok, fix = _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat)
+        if ok or fix is None or attempt == corrections:
+            return x, ok
+        nag, nau, nal = fix
+        if np.array_equal(nag, ag) and np.array_equal(nau, au) and np.array_equal(nal, al):
+            return x, False
+        ag, au, al = nag, nau, nal
+    return x, False
+
+
+def _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat):
+    """One polish on the active set (qp._polish_attempt in stage form)."""
     n = sq.n
     idl = 1.0 / POLISH_DELTA
-    dg = np.where(s < z, idl, 0.0)
-    dbu = np.where(su < zu, idl, 0.0) if boxed else np.zeros(n)
-    dbl = np.where(sl < zl, idl, 0.0) if boxed else np.zeros(n)
+    dg = np.where(ag, idl, 0.0)
+    dbu = np.where(au, idl, 0.0)
+    dbl = np.where(al, idl, 0.0)
     fac = sq.riccati_factor(dg, dbu + dbl)
-    ag = dg > 0
     x = np.zeros(n); xv = np.zeros((sq.N + 1, 4))
     yg = np.zeros(sq.p); yu = np.zeros(n); yl = np.zeros(n)
     for _ in range(POLISH_REFINE + 1):
@@ -285,20 +304,29 @@ def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat):
         yu = yu + dbu * (dx - ryu)
         yl = yl + dbl * (-dx - ryl)
         x = x + dx; xv = xv + dy
-    gx = sq.grow(sq.rollout(x))
+    gxw = sq.grow(sq.rollout(x)) - w
     wscale = 1.0 + max(np.abs(w).max() if len(w) else 0.0, np.maximum(np.abs(lb), np.abs(ub)).max() if boxed else 0.0)
-    viol = max((gx - w).max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
+    viol = max(gxw.max() if len(w) else -np.inf, (x - ub).max() if boxed else -np.inf,
                (lb - x).max() if boxed else -np.inf)
     part = sq.partner
-    yg_sign = yg
+    paired = np.zeros(len(yg), bool)
     if len(yg):
         paired = ag & (part >= 0) & ag[np.maximum(part, 0)]
-        yg_sign = np.where(paired, 0.0, yg)
+    yg_sign = np.where(paired, 0.0, yg)
     ymin = min(yg_sign.min() if len(yg) else 0.0, yu.min() if boxed else 0.0, yl.min() if boxed else 0.0)
     yscale = 1.0 + max(np.abs(yg).max() if len(yg) else 0.0, np.abs(yu).max() if boxed else 0.0,
                        np.abs(yl).max() if boxed else 0.0)
-    ok = bool(viol <= POLISH_TOL * wscale and ymin >= -POLISH_TOL * yscale and np.all(np.isfinite(x)))
-    return x, ok
+    finite = bool(np.all(np.isfinite(x)))
+    vtol, ytol = POLISH_TOL * wscale, -POLISH_TOL * yscale
+    ok = bool(viol <= vtol and ymin >= ytol and finite)
+    if ok or not finite:
+        return x, ok, None
+    nag = np.where(ag, ~(~paired & (yg < ytol)), gxw > vtol)
+    nau, nal = au, al
+    if boxed:
+        nau = np.where(au, ~(yu < ytol), x - ub > vtol)
+        nal = np.where(al, ~(yl < ytol), lb - x > vtol)
+    return x, ok, (nag, nau, nal)
 
 
 def solve_instance(asm, x0, xref=None, **kw):

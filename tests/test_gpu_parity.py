@@ -118,8 +118,10 @@ def test_golden_vectors(gpu_available, name, N, kernel):
         xN = (asm.T @ x0 + asm.S @ uu)[-4:]
         tA, tb = asm.term_A[:, -4:], asm.term_b
         assert (tA @ xN - tb).max() <= VIOL_TOL
-    # the IPM follows the oracle's iteration sequence to within a couple of steps
-    assert np.abs(it[ok] - g["iters"][ok]).max() <= 3
+    # the IPM follows the oracle's iteration sequence to within a couple of steps (the grouped kernel
+    # repeats a rejected polish on the corrected active set, the fallback kernels do not)
+    ref_it = g["iters"] if kernel == 7 else g["iters_single"]
+    assert np.abs(it[ok] - ref_it[ok]).max() <= 3
 
 
 def _random_x0(rng, goal_x, B):
@@ -156,6 +158,33 @@ def test_random_batch_vs_c_oracle(gpu_available, name, N, kernel):
         assert r["certified"]
         assert np.abs(u[i] - r["u_exact"]).max() <= U_TOL
         assert _violation(asm, X[i], u[i]) <= VIOL_TOL
+
+
+def test_polish_correction_round(gpu_available):
+    """A rejected polish is repeated once on the corrected active set (grouped kernel, and the oracle with
+    POLISH_CORRECTIONS = 1): on the instances where that changes the oracle's iteration count, the grouped
+    kernel follows the corrected sequence and the staged kernel (single attempt) the other one; statuses
+    and optima do not depend on it."""
+    import torch
+    from oracle.cpu import CpuProblem
+    asm, qp = _setup("RoadEnv", 20)
+    X = _random_x0(np.random.default_rng(77), asm.goal[0], 8192)
+    cp = CpuProblem(asm)
+    u1, s1, i1 = cp.solve(X)
+    u0, s0, i0 = cp.solve(X, polish_corrections=0)
+    np.testing.assert_array_equal(s0, s1)
+    differs = (s1 == 0) & (i0 != i1)
+    assert differs.sum() >= 100 and (i1[differs] < i0[differs]).all()
+    for kernel, ref, other in ((7, i1, i0), (2, i0, i1)):
+        u, st, it = qp.solve(torch.as_tensor(X).cuda(), settings=_settings(kernel))
+        u, st, it = u.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+        same = st == s1
+        assert same.mean() > 0.999                     # (boundary instances aside)
+        d = differs & same
+        assert (it[d] == ref[d]).mean() > 0.8, kernel
+        assert (it[d] == other[d]).mean() < 0.2, kernel
+        both = (st == 0) & (s1 == 0)
+        assert np.abs(u[both] - u1[both]).max() <= U_TOL
 
 
 def test_flags_and_edge_cases(gpu_available):

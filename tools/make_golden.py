@@ -111,6 +111,39 @@ def dump_constructor(ctrl, path, ref_mg):
                         term=np.hstack((tA[:, -4:], np.asarray(tb, float)[:, None])))
 
 
+def qp_vectors():
+    """qp_<env>_N<N>.npz: seeded x0 with the oracle's status, iteration counts (``iters``: with the
+    polish's correction round, ``iters_single``: single-attempt polish of the fallback kernels),
+    the certified optimum and the feasibility margin.  Needs the oracle and the reference's
+    terminal-set files only."""
+    for name, N in CONFIGS:
+        asm = oa.build(name, N, terminal_set_dir=os.path.join(REF, "terminal_sets"))
+
+        rng = np.random.default_rng(1000 + N + len(name))
+        X0 = sample_x0(rng, asm.goal[0], 64)
+        status, iters, iters1, ustar, margin = [], [], [], [], []
+        for x0 in X0:
+            r = oq.solve_instance(asm, x0)
+            r1 = oq.solve_instance(asm, x0, polish_corrections=0)
+            assert r1["status"] == r["status"]
+            Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
+            pre = pw - pE @ x0
+            m = float(pre.min()) if pre.size and pre.min() < 0 else oq.lp_margin(Gn, w0n - En @ x0, asm.lb, asm.ub)
+            if r["status"] == oq.STATUS_OPTIMAL:
+                assert r["certified"], (name, N, x0, r.get("kkt"))
+                ustar.append(r["u_exact"])
+            else:
+                ustar.append(np.full(2 * N, np.nan))
+            assert (m >= 0) == (r["status"] == oq.STATUS_OPTIMAL), (name, N, x0, m, r["status"])
+            status.append(r["status"]); iters.append(r["iters"]); iters1.append(r1["iters"]); margin.append(m)
+        np.savez(os.path.join(OUT, f"qp_{name}_N{N}.npz"), x0=X0, status=np.array(status, np.int32),
+                 iters=np.array(iters, np.int32), iters_single=np.array(iters1, np.int32), u_star=np.array(ustar),
+                 margin=np.array(margin))
+        print(name, N, "feasible", int(np.sum(np.array(status) == 0)), "/ 64",
+              "iters mean %.2f" % np.mean([i for i, s in zip(iters, status) if s == 0]),
+              "(single-attempt polish %.2f)" % np.mean([i for i, s in zip(iters1, status) if s == 0]))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref_mg, ref_env, ref_sim, ref_cfg, ref_mpc = import_reference()
@@ -165,28 +198,7 @@ def main():
              Bd=np.asarray(dfb.Bd, float), Cd=np.asarray(dfb.Cd, float), L1=dfb.L1, L2=np.asarray(dfb.L2, float),
              next_dist_x=np.array(dx), next_dist_d=np.array(dd))
 
-    for name, N in CONFIGS:
-        asm = oa.build(name, N, terminal_set_dir=os.path.join(REF, "terminal_sets"))
-
-        rng = np.random.default_rng(1000 + N + len(name))
-        X0 = sample_x0(rng, asm.goal[0], 64)
-        status, iters, ustar, margin = [], [], [], []
-        for x0 in X0:
-            r = oq.solve_instance(asm, x0)
-            Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
-            pre = pw - pE @ x0
-            m = float(pre.min()) if pre.size and pre.min() < 0 else oq.lp_margin(Gn, w0n - En @ x0, asm.lb, asm.ub)
-            if r["status"] == oq.STATUS_OPTIMAL:
-                assert r["certified"], (name, N, x0, r.get("kkt"))
-                ustar.append(r["u_exact"])
-            else:
-                ustar.append(np.full(2 * N, np.nan))
-            assert (m >= 0) == (r["status"] == oq.STATUS_OPTIMAL), (name, N, x0, m, r["status"])
-            status.append(r["status"]); iters.append(r["iters"]); margin.append(m)
-        np.savez(os.path.join(OUT, f"qp_{name}_N{N}.npz"), x0=X0, status=np.array(status, np.int32),
-                 iters=np.array(iters, np.int32), u_star=np.array(ustar), margin=np.array(margin))
-        print(name, N, "feasible", int(np.sum(np.array(status) == 0)), "/ 64",
-              "iters mean %.2f" % np.mean([i for i, s in zip(iters, status) if s == 0]))
+    qp_vectors()
 
     # plant golden: reference simulator on seeded pairs
     rng = np.random.default_rng(7)
@@ -263,4 +275,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--only-qp" in sys.argv:
+        qp_vectors()      # (the other fixtures do not depend on the solver's iteration sequence)
+    else:
+        main()
