@@ -214,8 +214,9 @@ struct MtH {
 //      and the group claims its next instance at once.  No polish code, no polish state.
 //   2  polish only, over the hand-off list: every instance runs the same fixed sequence (active-set
 //      factorization, solve, three refinements, acceptance test), so the four groups of a wave polish
-//      in lock-step instead of one at a time beside three iterating groups.  Rejected polishes go
-//      to the retry list.
+//      in lock-step instead of one at a time beside three iterating groups.  A group whose polish
+//      is rejected keeps the instance for the correction round (its next trip, see act_next); what
+//      is rejected again goes to the retry list.
 //   0  the complete algorithm in one kernel (iterations and polish interleaved per group): solves the
 //      retry list from scratch -- the arithmetic is deterministic, so this reproduces the rejected
 //      polish and carries on exactly as a single-kernel solve would -- and serves callers that bring
