@@ -111,6 +111,23 @@ def test_cpu_path_flags_fallback_and_edge_cases(tmp_path):
     np.testing.assert_array_equal(s1, s2)
 
 
+def test_cpu_path_iteration_limit():
+    """Small max_iter: last-resort polish and the max-iter status, identical to the oracle's."""
+    from oracle.cpu import CpuProblem
+    from carmpc_amd.qp import SolverSettings
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    X = _x0(np.random.default_rng(5), asm.goal[0], 512)
+    qp = _cpu_qp(asm)
+    for mi in (3, 7):
+        uc, sc, ic = CpuProblem(asm).solve(X, max_iter=mi, threads=4)
+        u, st, it = qp.solve(X, settings=SolverSettings(max_iter=mi), threads=4)
+        np.testing.assert_array_equal(st, sc)
+        np.testing.assert_array_equal(it, ic)
+        assert (st == 2).sum() > 50 and (st == 0).sum() > 20
+        both = st == 0
+        assert np.abs(u[both] - uc[both]).max() <= U_TOL
+
+
 def test_cpu_path_disturbance_offsets():
     asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
     qp = _cpu_qp(asm)

@@ -187,6 +187,36 @@ def test_polish_correction_round(gpu_available):
         assert np.abs(u[both] - u1[both]).max() <= U_TOL
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_iteration_limit(gpu_available, kernel):
+    """Small max_iter: the last-resort polish at the limit, and the max-iter status where it is rejected,
+    against the oracle -- in the single launch and (grouped kernel) in the three-launch form, where the
+    limit is reached in the iteration launch, polished in the second and reported by the third."""
+    import torch
+    from oracle.cpu import CpuProblem
+    from carmpc_amd.qp import SolverSettings
+    asm, qp = _setup("RoadMultipleCarsEnv", 20)
+    X = _random_x0(np.random.default_rng(5), asm.goal[0], 2048)
+    cp = CpuProblem(asm)
+    for mi in (3, 7):
+        uc, sc, ic = cp.solve(X, max_iter=mi, polish_corrections=1 if kernel == 7 else 0)
+        assert (sc == 2).sum() > 200 and (sc == 0).sum() > 100
+        u, st, it = qp.solve(torch.as_tensor(X).cuda(), settings=SolverSettings(max_iter=mi, kernel=kernel))
+        un, stn, itn = u.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()
+        assert (stn == sc).mean() > 0.995, (mi, np.bincount(stn, minlength=4), np.bincount(sc, minlength=4))
+        lim = (stn == 2) & (sc == 2)
+        assert (itn[lim] == mi).all() and (ic[lim] == mi).all()
+        both = (stn == 0) & (sc == 0)
+        assert np.abs(un[both] - uc[both]).max() <= U_TOL
+        if kernel == 7:
+            reps = 32                                   # 65,536 instances: the three-launch form
+            Xb = torch.as_tensor(np.tile(X, (reps, 1))).cuda()
+            ub, stb, itb = qp.solve(Xb, settings=SolverSettings(max_iter=mi, kernel=kernel))
+            assert torch.equal(stb, st.repeat(reps)) and torch.equal(itb, it.repeat(reps))
+            ok = (st == 0).repeat(reps)
+            assert torch.equal(ub[ok], u.repeat(reps, 1)[ok])
+
+
 def test_flags_and_edge_cases(gpu_available):
     import torch
     from oracle.cpu import CpuProblem
