@@ -46,7 +46,8 @@ KDESC = {1: "ipm_dense (wavefront per QP, G/H in LDS, dense normal matrix)",
          3: "ipm_dense, 4 waves per workgroup",
          7: "ipm_riccati (16 lanes per QP, 4 QPs per wavefront, row state in registers, stage-form Riccati "
             "factorization and solves on v_mfma_f64_4x4x4 with one matrix entry per lane, per-group instance "
-            "refill, one launch for all environments)"}
+            "refill; all environments per launch; large batches as three launches: iterations with hand-off, "
+            "lock-step polish with one correction round, single-kernel solve of the rejected rest)"}
 
 
 def sample_shard(rank: int, B: int, goals, seed: int = 5):
@@ -157,6 +158,11 @@ class GpuBackend:
     def __init__(self, args, local_rank):
         import torch
         self.torch = torch
+        ndev = torch.cuda.device_count()
+        if local_rank >= ndev > 0:      # more ranks than GPUs (a rehearsal of the N>1 flow on one GPU): share
+            print(f"bench: local rank {local_rank} shares GPU {local_rank % ndev} ({ndev} visible): "
+                  "throughput of this run is not a scaling number", file=sys.stderr)
+            local_rank %= ndev
         self.device = torch.device("cuda", local_rank)
         torch.cuda.set_device(self.device)
         self.stream = torch.cuda.current_stream()
