@@ -284,15 +284,17 @@ struct RicSegs {
 // single kernel), device memory for one call.  cnt holds kRicClaimStride words per segment: [0] claim
 // counter of round 0's iteration launch; for round r: [4r+1] number of handed-off instances, [4r+2]
 // claim counter of the polish launch, [4r+3] number of rejected polishes, [4r+4] claim counter of the
-// launch that takes them (round r+1's iterations, or the single kernel after the last round).  The index
-// lists are per segment, starting at the segment's first instance, and reused from round to round;
-// masks and iteration counts are stored per instance.  cnt null: no pipeline.
+// launch that takes them (round r+1's iterations, or the single kernel after the last round).  The lists
+// are per segment, starting at the segment's first instance, and reused from round to round.  A hand-off
+// is one 128-byte record (kRicRecWords 32-bit words, one cache line written by the iteration launch and
+// read by the polish launch): words 0..15 the lanes' active-set masks (bit s = row slot s active, bits
+// 16.. = box rows of the lane's inputs), 16..23 the instance's x0 (4 doubles), 24 the segment-relative
+// row, 25 the iterations done.  cnt null: no pipeline.
+constexpr int kRicRecWords = 32, kRicRecX0 = 16, kRicRecRow = 24, kRicRecIt = 25;
 struct RicWork {
     unsigned* cnt;
-    int32_t* pend_idx;    // total: segment-relative rows awaiting the polish
-    int32_t* pend_it;     // total: IPM iterations done at the hand-off
+    uint32_t* pend_rec;   // total x kRicRecWords: hand-off records in hand-off order
     int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
-    uint32_t* pend_mask;  // total x 16 lanes: bit s = row slot s active, bits 16.. = box rows of the owned inputs
     int32_t round;        // pipeline round of this launch
 };
 // One round measured best on the 131,072-instance mixed shard (11.45M QP/s; two rounds 10.9M): some 6 %

@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 S.claim = wc + 4 * W.round;
             }
         } else if constexpr (MODE == 2) {
-            S.index = W.pend_idx + seg0;
+            S.index = nullptr;   // (rows come from the hand-off records)
             S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round + 1);
             S.claim = wc + 4 * W.round + 2;
         } else {   // after the last round
@@ -946,7 +946,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     const int64_t nlive = S.count ? (int64_t)*S.count : batch;
     int64_t slot = S.claim ? claim() : ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
     bool live = slot < nlive;   // the group has an instance to work on
-    int64_t inst = live && S.index ? (int64_t)S.index[slot] : slot;
+    // slot -> row: the caller's list, the hand-off record (polish launch), or the slot itself
+    auto row_of = [&](int64_t sl, bool lv) -> int64_t {
+        if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(seg0 + sl) * kRicRecWords + kRicRecRow] : sl;
+        else return lv && S.index ? (int64_t)S.index[sl] : sl;
+    };
+    int64_t inst = row_of(slot, live);
     bool fresh = true;          // ... that still needs its initial point
     double s_[RS], z_[RS];
     double xs[2][4];
@@ -975,7 +980,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
         }
         slot = S.claim ? claim() : slot + stride;
         live = slot < nlive;
-        inst = live && S.index ? (int64_t)S.index[slot] : slot;
+        inst = row_of(slot, live);
         fresh = true;
     };
     RT_DECL
@@ -1012,7 +1017,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             double xv0[NX], xr[NX];
 #pragma unroll
             for (int k = 0; k < NX; ++k) {
-                xv0[k] = x0[inst * NX + k];
+                if constexpr (MODE == 2)
+                    xv0[k] = reinterpret_cast<const double*>(W.pend_rec + (seg0 + slot) * kRicRecWords + kRicRecX0)[k];
+                else
+                    xv0[k] = x0[inst * NX + k];
                 xr[k] = xref ? xref[inst * NX + k] : Igoal[k];
             }
             // x0-only rows (G_r = 0): preconditions
@@ -1318,11 +1326,15 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                                     m |= (BX(F_SU, sg, c) < BX(F_ZU, sg, c) ? 1u : 0u) << box_bit(sg, c, 0);
                                     m |= (BX(F_SL, sg, c) < BX(F_ZL, sg, c) ? 1u : 0u) << box_bit(sg, c, 1);
                                 }
-                        W.pend_mask[(seg0 + inst) * G16 + j] = m;
+                        unsigned pos = 0;
+                        if (j == 0) pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);
+                        pos = __shfl(pos, lane & ~(G16 - 1), 64);
+                        uint32_t* hrec = W.pend_rec + (seg0 + pos) * kRicRecWords;
+                        hrec[j] = m;
+                        if (j < NX) reinterpret_cast<double*>(hrec + kRicRecX0)[j] = x0[inst * NX + j];
                         if (j == 0) {
-                            W.pend_it[seg0 + inst] = it;
-                            const unsigned pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);
-                            W.pend_idx[seg0 + pos] = (int32_t)inst;
+                            hrec[kRicRecRow] = (uint32_t)inst;
+                            hrec[kRicRecIt] = (uint32_t)it;
                         }
                         finish(0, false, false);
                         active = false;
@@ -1335,8 +1347,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 // the hand-off record replaces residuals and decisions
                 polish = true;
                 if (active && !RIC_REPOL) {
-                    actm = W.pend_mask[(seg0 + inst) * G16 + j];
-                    it = W.pend_it[seg0 + inst];
+                    const uint32_t* hrec = W.pend_rec + (seg0 + slot) * kRicRecWords;
+                    actm = hrec[j];
+                    it = (int)hrec[kRicRecIt];
                 }
             }
             const bool any_polish = __any(polish);
@@ -1430,16 +1443,15 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
 hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                         int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
     const size_t n = (size_t)total, ncnt = (size_t)kRicClaimStride * kRicMaxSeg;
-    const size_t bytes = sizeof(unsigned) * ncnt + sizeof(int32_t) * 3 * n + sizeof(uint32_t) * kRicLanes * n;
+    const size_t bytes = sizeof(unsigned) * ncnt + sizeof(uint32_t) * kRicRecWords * n + sizeof(int32_t) * n;
+    static_assert(kRicLanes == kRicRecX0 && (kRicClaimStride * kRicMaxSeg * sizeof(unsigned)) % 128 == 0, "record layout");
     char* base = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&base), bytes, stream);
     if (e != hipSuccess) return e;
     RicWork W{};
     W.cnt = reinterpret_cast<unsigned*>(base);
-    W.pend_idx = reinterpret_cast<int32_t*>(W.cnt + ncnt);
-    W.pend_it = W.pend_idx + n;
-    W.retry_idx = W.pend_it + n;
-    W.pend_mask = reinterpret_cast<uint32_t*>(W.retry_idx + n);
+    W.pend_rec = reinterpret_cast<uint32_t*>(W.cnt + ncnt);   // (ncnt words = 256 bytes: records stay line-aligned)
+    W.retry_idx = reinterpret_cast<int32_t*>(W.pend_rec + (size_t)kRicRecWords * n);
     e = launch_zero_u32(W.cnt, (int)ncnt, stream);
     // rounds of (iterations, polish): round r takes the instances whose first r polishes were rejected
     // (a few per cent after round 0); what is left after the last round goes to the single kernel

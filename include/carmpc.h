@@ -141,7 +141,7 @@ int carmpc_problem_get(const carmpc_problem* prob, double* T, double* S, double*
  * Stream-ordered on `stream`.  Device memory beyond the arguments comes from the stream-ordered
  * allocator: a claim counter, and for large batches of the grouped kernel (which then runs as
  * an iteration launch, a polish launch and a launch for the instances whose polish was rejected)
- * the work lists between those launches, 76 bytes per instance.  Results do not depend on which
+ * the work lists between those launches, 132 bytes per instance.  Results do not depend on which
  * form ran. */
 int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
                        double* u_out, int32_t* status, int32_t* iters,
