@@ -297,12 +297,13 @@ struct RicWork {
     int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
     int32_t round;        // pipeline round of this launch
 };
-// One round measured best on the 131,072-instance mixed shard (11.45M QP/s; two rounds 10.9M): some 6 %
-// of the polishes are rejected, a second round solves those again with the lean kernels but still leaves
-// a latency-bound single-kernel tail for the ones rejected twice.
+// One round of (iterations, polish): a second one for the instances whose polish was rejected measured
+// slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 0.1 % since the
+// polish has its correction round) -- it solves them with the lean kernels but still leaves a latency-bound
+// single-kernel tail for the ones rejected again.
 constexpr int kRicRounds = 1;
 // smallest batch (instances of one call) solved by the pipeline: measured cross-over between 32,768 (single
-// kernel 8.5M QP/s, pipeline 8.2M) and 65,536 (9.1M, 9.8M) on RoadOneCarEnv, N = 20
+// kernel 10.1M QP/s, pipeline 10.0M) and 65,536 (10.6M, 11.5M) on RoadOneCarEnv, N = 20
 constexpr int kRicPipelineMin = 49152;
 static_assert(4 * kRicRounds < kRicClaimStride, "counter slots per segment");
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,

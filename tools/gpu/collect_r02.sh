@@ -1,5 +1,5 @@
 #!/bin/bash
-# measurement set of the round: bench lines of every configuration (with CPU baselines), per-instance and
+# measurement set: bench lines of every configuration (with CPU baselines), per-instance and
 # closed-loop rates, kernel trace + HBM counters of the default workload, kernel trace of config 4
 set -o pipefail
 cd $GRAFT_REPO_ROOT
