@@ -41,7 +41,8 @@ struct carmpc_cpu_problem {
 
 namespace {
 
-constexpr double kPolishMu = 1e-6, kPolishDelta = 1e-10, kPolishTol = 1e-11;
+constexpr double kPolishMu = 5e-5, kPolishRes = 3e-6;   // polish gate of the grouped device kernel (ipm_riccati.hip)
+constexpr double kPolishDelta = 1e-10, kPolishTol = 1e-11;
 constexpr int kPolishRefine = 3;
 constexpr int kPolishCorrections = 1;   // correction rounds of a rejected polish
 constexpr double kInf = std::numeric_limits<double>::infinity();
@@ -457,7 +458,9 @@ struct Solver {
             if (!std::isfinite(mu) || !std::isfinite(rdn)) { copy_u(u_out, u.data()); return CARMPC_NUMERICAL; }
             const bool res_ok = rpn <= tol * pscale && rdn <= tol * dscale;
             const bool last = it >= max_iter;
-            const bool do_polish = !polish_failed && ((res_ok && mu <= kPolishMu) || last);
+            const double ptol = std::max(kPolishRes, tol);
+            const bool pres_ok = rpn <= ptol * pscale && rdn <= ptol * dscale;
+            const bool do_polish = !polish_failed && ((pres_ok && mu <= kPolishMu) || last);
             if (!do_polish) {
                 if (last) { copy_u(u_out, u.data()); return CARMPC_MAX_ITER; }
                 if (res_ok && mu <= tol_mu) { copy_u(u_out, u.data()); return CARMPC_OPTIMAL; }

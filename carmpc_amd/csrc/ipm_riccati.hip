@@ -101,7 +101,21 @@ constexpr int REC = 20;   // doubles per stage record (160 B)
 //   [18..19] Db_t | kappa_t
 constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
 
-constexpr double POLISH_MU = 1e-6;
+// The polish is attempted once mu <= POLISH_MU with both residuals within POLISH_RES (relative, like the
+// termination tolerance): far earlier than the IPM would terminate.  An accepted polish is the exact
+// optimum whenever it comes, so the gate only trades iterations saved (about 1.5 per instance against the
+// conservative gate mu <= 1e-6, residuals within the termination tolerance) for more rejected attempts,
+// most of which the correction round repairs (measured: gates from 1e-6 / 1e-8 to 1e-3 / 1e-6, best
+// between 5e-5 / 3e-6 and 1e-4 / 3e-6 on every workload).  Overridable for such sweeps (tools/gpu/mkvar.sh).
+// The per-instance kernels keep the conservative gate, like the fallback kernels.
+#ifndef CARMPC_POLISH_MU
+#define CARMPC_POLISH_MU 5e-5
+#endif
+#ifndef CARMPC_POLISH_RES
+#define CARMPC_POLISH_RES 3e-6
+#endif
+constexpr double POLISH_MU = CARMPC_POLISH_MU, POLISH_RES = CARMPC_POLISH_RES;
+constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
 constexpr double POLISH_DELTA = 1e-10;
 constexpr int POLISH_REFINE = 3;
 constexpr double POLISH_TOL = 1e-11;
@@ -1291,7 +1305,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 } else {
                     const bool res_ok = rpn <= S.tol * pscale && rdn <= S.tol * dscale;
                     const bool last = it >= S.max_iter;
-                    polish = !polish_failed && ((res_ok && mu <= POLISH_MU) || last);
+                    const double ptol = HET ? S.tol : fmax(POLISH_RES, S.tol);
+                    const bool pres_ok = rpn <= ptol * pscale && rdn <= ptol * dscale;
+                    polish = !polish_failed && ((pres_ok && mu <= (HET ? POLISH_MU_CONSERVATIVE : POLISH_MU)) || last);
                     if constexpr (MODE != 2) {
                         // round r of the pipeline (the single kernel after the last round included): the
                         // instance's first r polishes are known to be rejected -- that is why it is here;

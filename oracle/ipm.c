@@ -28,7 +28,8 @@
 #define UNBOXED_BOUND 1e9
 #define PRE_TOL 1e-9
 #define STEP_FRAC 0.99
-#define POLISH_MU 1e-6
+#define POLISH_MU 5e-5    /* polish gate: mu <= POLISH_MU and residuals within max(POLISH_RES, tol) */
+#define POLISH_RES 3e-6
 #define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
 #define POLISH_REFINE 3
@@ -109,7 +110,11 @@ static void gtmul(const qp_t* P, const double* y, double* out) { /* out = G' y *
 
 /* correction rounds of a rejected polish (qp.POLISH_CORRECTIONS); 0 = the single-attempt polish */
 static int g_polish_corrections = 1;
-void oracle_set_polish_corrections(int k) { g_polish_corrections = k; }
+static double g_polish_mu = POLISH_MU, g_polish_res = POLISH_RES;
+/* qp.FALLBACK_POLISH = (0, 1e-6, 0): the single-attempt polish behind the conservative gate */
+void oracle_set_polish(int corrections, double mu, double res) {
+    g_polish_corrections = corrections; g_polish_mu = mu; g_polish_res = res;
+}
 
 typedef struct {   /* per-thread scratch */
     double *M, *s, *z, *rp, *ds, *dz, *dsa, *dza, *t, *rc, *gv, *pv1, *pv2;
@@ -326,7 +331,9 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
         if (1.0 + gzn > dscale) dscale = 1.0 + gzn;
         if (!isfinite(mu) || !isfinite(rdn)) { status = 3; break; }
         const int res_ok = rpn <= tol * pscale && rdn <= tol * dscale;
-        if (res_ok && mu <= POLISH_MU && polish(P, q, w, W, xpol)) {
+        const double ptol = g_polish_res > tol ? g_polish_res : tol;
+        const int pres_ok = rpn <= ptol * pscale && rdn <= ptol * dscale;
+        if (pres_ok && mu <= g_polish_mu && polish(P, q, w, W, xpol)) {
             memcpy(u, xpol, sizeof(double) * n);
             status = 0;
             break;

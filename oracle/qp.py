@@ -33,7 +33,12 @@ MAX_ITER = 60
 STEP_FRAC = 0.99
 REFINE = 1                 # iterative-refinement passes on the corrector direction
 REFINE_MU = 1e-6           # ... only once mu <= REFINE_MU (D = z/s spans many decades)
-POLISH_MU = 1e-6           # attempt the active-set polish once mu <= POLISH_MU (and residuals ok)
+POLISH_MU = 5e-5           # attempt the active-set polish once mu <= POLISH_MU ...
+POLISH_RES = 3e-6          # ... and both residuals are within max(POLISH_RES, tol), relative.  An accepted
+#                            polish is the exact optimum whenever it comes; the gate trades iterations for
+#                            rejected attempts (most are repaired by the correction round).
+# the variant the fallback kernels (dense, staged, per-instance) run: single attempt, conservative gate
+FALLBACK_POLISH = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 3          # iterative-refinement passes of the polish
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
@@ -77,7 +82,8 @@ def opposite_pairs(G, w0, E):
 
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
-        trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None):
+        trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None,
+        polish_mu=None, polish_res=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -127,7 +133,9 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
             trace.append((it, mu, rpn, rdn))
         if not np.isfinite(mu) or not np.isfinite(rdn):
             return u, STATUS_NUMERICAL, it, z
-        if polish and rpn <= tol * pscale and rdn <= tol * dscale and mu <= POLISH_MU:
+        ptol = max(POLISH_RES if polish_res is None else polish_res, tol)
+        pmu = POLISH_MU if polish_mu is None else polish_mu
+        if polish and rpn <= ptol * pscale and rdn <= ptol * dscale and mu <= pmu:
             up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
                                  partner=partner, corrections=polish_corrections)
             if info is not None:

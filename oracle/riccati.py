@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
+from .qp import (MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -149,7 +149,8 @@ def _chol2_solve(L, b):
     return np.array([x0, x1]) if b.ndim == 1 else np.vstack([x0, x1])
 
 
-def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None):
+def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None,
+        polish_mu=None, polish_res=None):
     """qp.ipm + qp.polish_step in stage form for one instance.  Returns (u, status, iters)."""
     x0 = np.asarray(x0, float)
     xref = np.asarray(xref, float)
@@ -199,7 +200,9 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
             return u, STATUS_NUMERICAL, it
         res_ok = rpn <= tol * pscale and rdn <= tol * dscale
         last = it >= max_iter
-        polish = not polish_failed and ((res_ok and mu <= POLISH_MU) or last)
+        ptol = max(POLISH_RES if polish_res is None else polish_res, tol)
+        pres_ok = rpn <= ptol * pscale and rdn <= ptol * dscale
+        polish = not polish_failed and ((pres_ok and mu <= (POLISH_MU if polish_mu is None else polish_mu)) or last)
         if not polish:
             if last:
                 return u, STATUS_MAXITER, it

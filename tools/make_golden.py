@@ -113,7 +113,8 @@ def dump_constructor(ctrl, path, ref_mg):
 
 def qp_vectors():
     """qp_<env>_N<N>.npz: seeded x0 with the oracle's status, iteration counts (``iters``: with the
-    polish's correction round, ``iters_single``: single-attempt polish of the fallback kernels),
+    oracle's polish -- early gate, correction round; ``iters_single``: the fallback kernels' variant,
+    qp.FALLBACK_POLISH),
     the certified optimum and the feasibility margin.  Needs the oracle and the reference's
     terminal-set files only."""
     for name, N in CONFIGS:
@@ -124,7 +125,7 @@ def qp_vectors():
         status, iters, iters1, ustar, margin = [], [], [], [], []
         for x0 in X0:
             r = oq.solve_instance(asm, x0)
-            r1 = oq.solve_instance(asm, x0, polish_corrections=0)
+            r1 = oq.solve_instance(asm, x0, **oq.FALLBACK_POLISH)
             assert r1["status"] == r["status"]
             Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
             pre = pw - pE @ x0
@@ -141,7 +142,7 @@ def qp_vectors():
                  margin=np.array(margin))
         print(name, N, "feasible", int(np.sum(np.array(status) == 0)), "/ 64",
               "iters mean %.2f" % np.mean([i for i, s in zip(iters, status) if s == 0]),
-              "(single-attempt polish %.2f)" % np.mean([i for i, s in zip(iters1, status) if s == 0]))
+              "(fallback polish variant %.2f)" % np.mean([i for i, s in zip(iters1, status) if s == 0]))
 
 
 def main():
