@@ -298,9 +298,9 @@ struct RicWork {
     int32_t round;        // pipeline round of this launch
 };
 // One round of (iterations, polish): a second one for the instances whose polish was rejected measured
-// slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 0.1 % since the
-// polish has its correction round) -- it solves them with the lean kernels but still leaves a latency-bound
-// single-kernel tail for the ones rejected again.
+// slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 1.5 % with the
+// correction round and the early polish gate) -- it solves them with the lean kernels but still leaves a
+// latency-bound single-kernel tail for the ones rejected again.
 constexpr int kRicRounds = 1;
 // smallest batch (instances of one call) solved by the pipeline: measured cross-over between 32,768 (single
 // kernel 10.1M QP/s, pipeline 10.0M) and 65,536 (10.6M, 11.5M) on RoadOneCarEnv, N = 20
