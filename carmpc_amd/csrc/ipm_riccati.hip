@@ -116,6 +116,16 @@ constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
 #endif
 constexpr double POLISH_MU = CARMPC_POLISH_MU, POLISH_RES = CARMPC_POLISH_RES;
 constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
+// Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path z = INIT_MU0 / s --
+// a centred start well inside the cone, about 1.1 iterations fewer than z = 1 with the floor at 1 (measured
+// plateau: INIT_MU0 60..100, INIT_SFLOOR 1.5..3).  INIT_MU0 = 0 means z = 1 (the per-instance kernels, like
+// the fallback kernels).
+#ifndef CARMPC_INIT_MU0
+#define CARMPC_INIT_MU0 100.0
+#endif
+#ifndef CARMPC_INIT_SFLOOR
+#define CARMPC_INIT_SFLOOR 2.0
+#endif
 constexpr double POLISH_DELTA = 1e-10;
 constexpr int POLISH_REFINE = 3;
 constexpr double POLISH_TOL = 1e-11;
@@ -242,6 +252,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                                                                int32_t* __restrict__ status_all,
                                                                int32_t* __restrict__ iters_all, Settings S_all) {
     static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
+    constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
     constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
@@ -1085,10 +1096,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         const double u0 = bx ? fmin(fmax(0.0, lb), ub) : 0.0;
                         BX(F_Q, sg, c) = own[sg] ? q : 0.0;
                         BX(F_U, sg, c) = u0;
-                        BX(F_SU, sg, c) = bx ? fmax(ub - u0, 1.0) : 1.0;
-                        BX(F_SL, sg, c) = bx ? fmax(u0 - lb, 1.0) : 1.0;
-                        BX(F_ZU, sg, c) = bx ? 1.0 : 0.0;
-                        BX(F_ZL, sg, c) = bx ? 1.0 : 0.0;
+                        const double su0 = fmax(ub - u0, kSFloor), sl0 = fmax(u0 - lb, kSFloor);
+                        BX(F_SU, sg, c) = bx ? su0 : 1.0;
+                        BX(F_SL, sg, c) = bx ? sl0 : 1.0;
+                        BX(F_ZU, sg, c) = bx ? (kMu0 > 0.0 ? kMu0 / su0 : 1.0) : 0.0;
+                        BX(F_ZL, sg, c) = bx ? (kMu0 > 0.0 ? kMu0 / sl0 : 1.0) : 0.0;
                         bn = bx ? fmax(bn, fmax(fabs(lb), fabs(ub))) : bn;
                         qn = fmax(qn, own[sg] ? fabs(q) : 0.0);
                         u0n = fmax(u0n, fabs(u0));
@@ -1114,8 +1126,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     const int sg = s / RSEG;
                     double c[4];
                     cf(s, c);
-                    s_[s] = valid(s) ? fmax(wv.w[s][lane] - dot4(c, xs[sg]), 1.0) : 1.0;
-                    z_[s] = valid(s) ? 1.0 : 0.0;
+                    const double s0 = fmax(wv.w[s][lane] - dot4(c, xs[sg]), kSFloor);
+                    s_[s] = valid(s) ? s0 : 1.0;
+                    z_[s] = valid(s) ? (kMu0 > 0.0 ? kMu0 / s0 : 1.0) : 0.0;
                 }
                 }
                 bnorm = 1.0 + row_max(bn);

@@ -30,6 +30,8 @@
 #define STEP_FRAC 0.99
 #define POLISH_MU 5e-5    /* polish gate: mu <= POLISH_MU and residuals within max(POLISH_RES, tol) */
 #define POLISH_RES 3e-6
+#define INIT_MU0 100.0     /* initial point: s = max(w - G u0, INIT_SFLOOR), z = INIT_MU0 / s (qp.py) */
+#define INIT_SFLOOR 2.0
 #define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
 #define POLISH_REFINE 3
@@ -111,9 +113,12 @@ static void gtmul(const qp_t* P, const double* y, double* out) { /* out = G' y *
 /* correction rounds of a rejected polish (qp.POLISH_CORRECTIONS); 0 = the single-attempt polish */
 static int g_polish_corrections = 1;
 static double g_polish_mu = POLISH_MU, g_polish_res = POLISH_RES;
-/* qp.FALLBACK_POLISH = (0, 1e-6, 0): the single-attempt polish behind the conservative gate */
-void oracle_set_polish(int corrections, double mu, double res) {
+static double g_init_mu0 = INIT_MU0, g_init_sfloor = INIT_SFLOOR;
+/* qp.FALLBACK_VARIANT = (0, 1e-6, 0, 0, 1): the single-attempt polish behind the conservative gate, z = 1
+ * and slack floor 1 at the start */
+void oracle_set_variant(int corrections, double mu, double res, double init_mu0, double init_sfloor) {
     g_polish_corrections = corrections; g_polish_mu = mu; g_polish_res = res;
+    g_init_mu0 = init_mu0; g_init_sfloor = init_sfloor;
 }
 
 typedef struct {   /* per-thread scratch */
@@ -276,8 +281,8 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
     gmul(P, u, W->gv);
     for (int r = 0; r < p; ++r) {
         double sv = w[r] - W->gv[r];
-        s[r] = sv > 1.0 ? sv : 1.0;
-        z[r] = 1.0;
+        s[r] = sv > g_init_sfloor ? sv : g_init_sfloor;
+        z[r] = g_init_mu0 > 0.0 ? g_init_mu0 / s[r] : 1.0;
         if (fabs(w[r]) > bnorm) bnorm = fabs(w[r]);
     }
     for (int i = 0; i < n; ++i) {
@@ -285,8 +290,9 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
         zu[i] = zl[i] = boxed ? 1.0 : 0.0;
         if (boxed) {
             double a = ub[i] - u[i], b = u[i] - lb[i];
-            su[i] = a > 1.0 ? a : 1.0;
-            sl[i] = b > 1.0 ? b : 1.0;
+            su[i] = a > g_init_sfloor ? a : g_init_sfloor;
+            sl[i] = b > g_init_sfloor ? b : g_init_sfloor;
+            if (g_init_mu0 > 0.0) { zu[i] = g_init_mu0 / su[i]; zl[i] = g_init_mu0 / sl[i]; }
             if (fabs(ub[i]) > bnorm) bnorm = fabs(ub[i]);
             if (fabs(lb[i]) > bnorm) bnorm = fabs(lb[i]);
         }

@@ -37,8 +37,14 @@ POLISH_MU = 5e-5           # attempt the active-set polish once mu <= POLISH_MU 
 POLISH_RES = 3e-6          # ... and both residuals are within max(POLISH_RES, tol), relative.  An accepted
 #                            polish is the exact optimum whenever it comes; the gate trades iterations for
 #                            rejected attempts (most are repaired by the correction round).
-# the variant the fallback kernels (dense, staged, per-instance) run: single attempt, conservative gate
-FALLBACK_POLISH = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0)
+# Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path, z = INIT_MU0 / s
+# (a centred start well inside the cone: about 1.1 iterations fewer than z = 1 with the floor at 1; measured
+# plateau for INIT_MU0 in 60..100 and INIT_SFLOOR in 1.5..3 on all four configurations).
+INIT_MU0 = 100.0
+INIT_SFLOOR = 2.0
+# the variant the fallback kernels (dense, staged, per-instance) run: z = 1 and slack floor 1 at the start,
+# one polish attempt behind the conservative gate
+FALLBACK_VARIANT = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0, init_mu0=0.0, init_sfloor=1.0)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 3          # iterative-refinement passes of the polish
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
@@ -83,7 +89,7 @@ def opposite_pairs(G, w0, E):
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
         trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None,
-        polish_mu=None, polish_res=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -101,12 +107,15 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         u = np.zeros(n)
     nb = n if boxed else 0
     m = p + 2 * nb
-    s = np.maximum(w - G @ u, 1.0); z = np.ones(p)
+    mu0 = INIT_MU0 if init_mu0 is None else init_mu0
+    sfl = INIT_SFLOOR if init_sfloor is None else init_sfloor
+    s = np.maximum(w - G @ u, sfl); z = mu0 / s if mu0 > 0 else np.ones(p)
     if boxed:
-        su = np.maximum(ub - u, 1.0); sl = np.maximum(u - lb, 1.0)
+        su = np.maximum(ub - u, sfl); sl = np.maximum(u - lb, sfl)
     else:
         su = np.ones(0); sl = np.ones(0)
-    zu = np.ones(nb); zl = np.ones(nb)
+    zu = mu0 / su if mu0 > 0 else np.ones(nb)
+    zl = mu0 / sl if mu0 > 0 else np.ones(nb)
     bnorm = 1.0 + max(np.abs(w).max() if p else 0.0,
                       np.abs(ub).max() if boxed else 0.0, np.abs(lb).max() if boxed else 0.0)
     qnorm = 1.0 + (np.abs(q).max() if n else 0.0)

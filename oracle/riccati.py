@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
+from .qp import (INIT_MU0, INIT_SFLOOR, MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -150,7 +150,7 @@ def _chol2_solve(L, b):
 
 
 def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None,
-        polish_mu=None, polish_res=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None):
     """qp.ipm + qp.polish_step in stage form for one instance.  Returns (u, status, iters)."""
     x0 = np.asarray(x0, float)
     xref = np.asarray(xref, float)
@@ -170,11 +170,13 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
         return (R @ v.reshape(-1, 2).T).T.reshape(-1)
 
     u = np.clip(np.zeros(n), lb, ub) if boxed else np.zeros(n)
-    s = np.maximum(w - sq.grow(sq.rollout(u)), 1.0); z = np.ones(p)
-    su = np.maximum(ub - u, 1.0) if boxed else np.ones(n)
-    sl = np.maximum(u - lb, 1.0) if boxed else np.ones(n)
-    zu = np.ones(n) if boxed else np.zeros(n)
-    zl = zu.copy()
+    mu0 = INIT_MU0 if init_mu0 is None else init_mu0
+    sfl = INIT_SFLOOR if init_sfloor is None else init_sfloor
+    s = np.maximum(w - sq.grow(sq.rollout(u)), sfl); z = mu0 / s if mu0 > 0 else np.ones(p)
+    su = np.maximum(ub - u, sfl) if boxed else np.ones(n)
+    sl = np.maximum(u - lb, sfl) if boxed else np.ones(n)
+    zu = (mu0 / su if mu0 > 0 else np.ones(n)) if boxed else np.zeros(n)
+    zl = (mu0 / sl if mu0 > 0 else np.ones(n)) if boxed else np.zeros(n)
     bmask = 1.0 if boxed else 0.0
     bnorm = 1.0 + max(np.abs(w).max() if p else 0.0, np.maximum(np.abs(lb), np.abs(ub)).max() if boxed else 0.0)
     qnorm = 1.0 + np.abs(q).max()

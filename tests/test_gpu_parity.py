@@ -119,7 +119,7 @@ def test_golden_vectors(gpu_available, name, N, kernel):
         tA, tb = asm.term_A[:, -4:], asm.term_b
         assert (tA @ xN - tb).max() <= VIOL_TOL
     # the IPM follows the oracle's iteration sequence to within a couple of steps (the grouped kernel runs
-    # the oracle's polish -- early gate, correction round --, the fallback kernels qp.FALLBACK_POLISH)
+    # the oracle's polish -- early gate, correction round --, the fallback kernels qp.FALLBACK_VARIANT)
     ref_it = g["iters"] if kernel == 7 else g["iters_single"]
     assert np.abs(it[ok] - ref_it[ok]).max() <= 3
 
@@ -162,7 +162,7 @@ def test_random_batch_vs_c_oracle(gpu_available, name, N, kernel):
 
 def test_polish_variants(gpu_available):
     """The grouped kernel runs the oracle's polish (attempted early -- qp.POLISH_MU / POLISH_RES -- and repeated
-    once on the corrected active set), the staged kernel the fallback variant (qp.FALLBACK_POLISH: one
+    once on the corrected active set), the staged kernel the fallback variant (qp.FALLBACK_VARIANT: one
     attempt behind the conservative gate).  Each follows its own oracle iteration sequence; statuses and
     optima do not depend on the variant."""
     import torch
@@ -172,7 +172,7 @@ def test_polish_variants(gpu_available):
     X = _random_x0(np.random.default_rng(77), asm.goal[0], 8192)
     cp = CpuProblem(asm)
     u1, s1, i1 = cp.solve(X)
-    u0, s0, i0 = cp.solve(X, **oq.FALLBACK_POLISH)
+    u0, s0, i0 = cp.solve(X, **oq.FALLBACK_VARIANT)
     np.testing.assert_array_equal(s0, s1)
     opt = s1 == 0
     assert np.abs(u1[opt] - u0[opt]).max() <= U_TOL
@@ -202,8 +202,8 @@ def test_iteration_limit(gpu_available, kernel):
     asm, qp = _setup("RoadMultipleCarsEnv", 20)
     X = _random_x0(np.random.default_rng(5), asm.goal[0], 2048)
     cp = CpuProblem(asm)
-    for mi in (3, 7):
-        uc, sc, ic = cp.solve(X, max_iter=mi, **({} if kernel == 7 else oq.FALLBACK_POLISH))
+    for mi in (5, 7):
+        uc, sc, ic = cp.solve(X, max_iter=mi, **({} if kernel == 7 else oq.FALLBACK_VARIANT))
         assert (sc == 2).sum() > 200 and (sc == 0).sum() > 100
         u, st, it = qp.solve(torch.as_tensor(X).cuda(), settings=SolverSettings(max_iter=mi, kernel=kernel))
         un, stn, itn = u.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()

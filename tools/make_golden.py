@@ -114,7 +114,7 @@ def dump_constructor(ctrl, path, ref_mg):
 def qp_vectors():
     """qp_<env>_N<N>.npz: seeded x0 with the oracle's status, iteration counts (``iters``: with the
     oracle's polish -- early gate, correction round; ``iters_single``: the fallback kernels' variant,
-    qp.FALLBACK_POLISH),
+    qp.FALLBACK_VARIANT),
     the certified optimum and the feasibility margin.  Needs the oracle and the reference's
     terminal-set files only."""
     for name, N in CONFIGS:
@@ -125,7 +125,7 @@ def qp_vectors():
         status, iters, iters1, ustar, margin = [], [], [], [], []
         for x0 in X0:
             r = oq.solve_instance(asm, x0)
-            r1 = oq.solve_instance(asm, x0, **oq.FALLBACK_POLISH)
+            r1 = oq.solve_instance(asm, x0, **oq.FALLBACK_VARIANT)
             assert r1["status"] == r["status"]
             Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
             pre = pw - pE @ x0
