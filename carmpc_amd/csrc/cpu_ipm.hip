@@ -43,7 +43,8 @@ namespace {
 
 constexpr double kPolishMu = 5e-5, kPolishRes = 3e-6;   // polish gate of the grouped device kernel (ipm_riccati.hip)
 constexpr double kPolishDelta = 1e-10, kPolishTol = 1e-11;
-constexpr double kInitMu0 = 100.0, kInitSFloor = 2.0;   // initial point s = max(w - G u0, floor), z = mu0 / s (ipm_riccati.hip)
+// initial point s = max(w - G u0, floor), z = mu0 / s, mu0 = clamp((|q|_inf / (kInitQPerVar n))^2, kInitMuMin, kInitMu0) (ipm_riccati.hip)
+constexpr double kInitMu0 = 100.0, kInitSFloor = 2.0, kInitMuMin = 1.0, kInitQPerVar = 3.5;
 constexpr int kPolishRefine = 3;
 constexpr int kPolishCorrections = 1;   // correction rounds of a rejected polish
 constexpr double kInf = std::numeric_limits<double>::infinity();
@@ -410,8 +411,7 @@ struct Solver {
             u[i] = boxed ? std::min(std::max(0.0, lbv[i]), ubv[i]) : 0.0;
             su[i] = boxed ? std::max(ubv[i] - u[i], kInitSFloor) : 1.0;
             sl[i] = boxed ? std::max(u[i] - lbv[i], kInitSFloor) : 1.0;
-            zu[i] = boxed ? kInitMu0 / su[i] : 0.0;
-            zl[i] = boxed ? kInitMu0 / sl[i] : 0.0;
+            zu[i] = zl[i] = bm;
         }
         for (int r = 0; r < p; ++r) {
             double vv = P.w0[r];
@@ -421,7 +421,10 @@ struct Solver {
         }
         rollout(u.data(), xs.data());
         grow(xs.data(), gu.data());
-        for (int r = 0; r < p; ++r) { s[r] = std::max(w[r] - gu[r], kInitSFloor); z[r] = kInitMu0 / s[r]; }
+        const double qrel = (1.0 / (kInitQPerVar * n)) * amax(q.data(), n);
+        const double mu0 = std::min(kInitMu0, std::max(kInitMuMin, qrel * qrel));
+        for (int r = 0; r < p; ++r) { s[r] = std::max(w[r] - gu[r], kInitSFloor); z[r] = mu0 / s[r]; }
+        for (int i = 0; i < n && boxed; ++i) { zu[i] = mu0 / su[i]; zl[i] = mu0 / sl[i]; }
         const int m = p + (boxed ? 2 * n : 0);
         const double inv_m = 1.0 / std::max(m, 1);
         double bnd = 0.0;

@@ -116,12 +116,23 @@ constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
 #endif
 constexpr double POLISH_MU = CARMPC_POLISH_MU, POLISH_RES = CARMPC_POLISH_RES;
 constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
-// Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path z = INIT_MU0 / s --
-// a centred start well inside the cone, about 1.1 iterations fewer than z = 1 with the floor at 1 (measured
-// plateau: INIT_MU0 60..100, INIT_SFLOOR 1.5..3).  INIT_MU0 = 0 means z = 1 (the per-instance kernels, like
-// the fallback kernels).
+// Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path z = mu0 / s with
+// mu0 = clamp((|q|_inf / (INIT_Q_PER_VAR n))^2, INIT_MU_MIN, INIT_MU0): a centred start whose distance from the
+// boundary follows the size of the linear term.  States far from the goal (large q, many active rows at the
+// optimum) start well inside the cone -- about 1.3 iterations fewer than z = 1 with the floor at 1 on the
+// bench's states --, states on closed-loop trajectories and near the goal (little or nothing active) start
+// close to the boundary and keep their 3 to 4 iterations, where a fixed mu0 = 100 costs them 5 (measured:
+// linear and quadratic rules; the best scale is 100..200 at N = 20, 50..70 at N = 10, about 35 at N = 5, hence
+// proportional to the number of variables).  INIT_MU0 = 0 means z = 1 (the per-instance kernels, like the
+// fallback kernels).
 #ifndef CARMPC_INIT_MU0
 #define CARMPC_INIT_MU0 100.0
+#endif
+#ifndef CARMPC_INIT_MU_MIN
+#define CARMPC_INIT_MU_MIN 1.0
+#endif
+#ifndef CARMPC_INIT_Q_PER_VAR
+#define CARMPC_INIT_Q_PER_VAR 3.5
 #endif
 #ifndef CARMPC_INIT_SFLOOR
 #define CARMPC_INIT_SFLOOR 2.0
@@ -253,6 +264,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                                                                int32_t* __restrict__ iters_all, Settings S_all) {
     static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
     constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
+    constexpr double kMuMin = CARMPC_INIT_MU_MIN, kQInv = 1.0 / (CARMPC_INIT_Q_PER_VAR * 2 * N);
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
     constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
@@ -1099,11 +1111,27 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         const double su0 = fmax(ub - u0, kSFloor), sl0 = fmax(u0 - lb, kSFloor);
                         BX(F_SU, sg, c) = bx ? su0 : 1.0;
                         BX(F_SL, sg, c) = bx ? sl0 : 1.0;
-                        BX(F_ZU, sg, c) = bx ? (kMu0 > 0.0 ? kMu0 / su0 : 1.0) : 0.0;
-                        BX(F_ZL, sg, c) = bx ? (kMu0 > 0.0 ? kMu0 / sl0 : 1.0) : 0.0;
+                        BX(F_ZU, sg, c) = bx ? 1.0 : 0.0;
+                        BX(F_ZL, sg, c) = bx ? 1.0 : 0.0;
                         bn = bx ? fmax(bn, fmax(fabs(lb), fabs(ub))) : bn;
                         qn = fmax(qn, own[sg] ? fabs(q) : 0.0);
                         u0n = fmax(u0n, fabs(u0));
+                    }
+                }
+                // multipliers on the central path: z = mu0 / s with mu0 following the size of the linear term
+                double mu0 = 0.0;
+                if constexpr (!HET && MODE != 2) {
+                    if (kMu0 > 0.0) {
+                        const double qrel = kQInv * row_max(qn);
+                        mu0 = fmin(kMu0, fmax(kMuMin, qrel * qrel));
+#pragma unroll
+                        for (int sg = 0; sg < 2; ++sg)
+#pragma unroll
+                            for (int c = 0; c < 2; ++c)
+                                if (own[sg] && boxed) {
+                                    BX(F_ZU, sg, c) = mu0 / BX(F_SU, sg, c);
+                                    BX(F_ZL, sg, c) = mu0 / BX(F_SL, sg, c);
+                                }
                     }
                 }
                 if constexpr (MODE != 2) {   // the polish starts from the active set alone
@@ -1128,7 +1156,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     cf(s, c);
                     const double s0 = fmax(wv.w[s][lane] - dot4(c, xs[sg]), kSFloor);
                     s_[s] = valid(s) ? s0 : 1.0;
-                    z_[s] = valid(s) ? (kMu0 > 0.0 ? kMu0 / s0 : 1.0) : 0.0;
+                    z_[s] = valid(s) ? (mu0 > 0.0 ? mu0 / s0 : 1.0) : 0.0;
                 }
                 }
                 bnorm = 1.0 + row_max(bn);

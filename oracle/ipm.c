@@ -32,6 +32,8 @@
 #define POLISH_RES 3e-6
 #define INIT_MU0 100.0     /* initial point: s = max(w - G u0, INIT_SFLOOR), z = INIT_MU0 / s (qp.py) */
 #define INIT_SFLOOR 2.0
+#define INIT_MU_MIN 1.0     /* mu0 = clamp((|q|_inf / (INIT_Q_PER_VAR n))^2, INIT_MU_MIN, INIT_MU0) */
+#define INIT_Q_PER_VAR 3.5
 #define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
 #define POLISH_REFINE 3
@@ -278,11 +280,20 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
         u[i] = v;
     }
     double bnorm = 0.0, qnorm = 0.0;
+    double mu0 = g_init_mu0;
+    if (mu0 > 0.0) {
+        double qn = 0.0;
+        for (int i = 0; i < n; ++i) if (fabs(q[i]) > qn) qn = fabs(q[i]);
+        double m = (1.0 / (INIT_Q_PER_VAR * n)) * qn;
+        m = m * m;
+        if (m < INIT_MU_MIN) m = INIT_MU_MIN;
+        if (m < mu0) mu0 = m;
+    }
     gmul(P, u, W->gv);
     for (int r = 0; r < p; ++r) {
         double sv = w[r] - W->gv[r];
         s[r] = sv > g_init_sfloor ? sv : g_init_sfloor;
-        z[r] = g_init_mu0 > 0.0 ? g_init_mu0 / s[r] : 1.0;
+        z[r] = mu0 > 0.0 ? mu0 / s[r] : 1.0;
         if (fabs(w[r]) > bnorm) bnorm = fabs(w[r]);
     }
     for (int i = 0; i < n; ++i) {
@@ -292,7 +303,7 @@ static int solve_one(const qp_t* P, const double* q, const double* w, double* u,
             double a = ub[i] - u[i], b = u[i] - lb[i];
             su[i] = a > g_init_sfloor ? a : g_init_sfloor;
             sl[i] = b > g_init_sfloor ? b : g_init_sfloor;
-            if (g_init_mu0 > 0.0) { zu[i] = g_init_mu0 / su[i]; zl[i] = g_init_mu0 / sl[i]; }
+            if (mu0 > 0.0) { zu[i] = mu0 / su[i]; zl[i] = mu0 / sl[i]; }
             if (fabs(ub[i]) > bnorm) bnorm = fabs(ub[i]);
             if (fabs(lb[i]) > bnorm) bnorm = fabs(lb[i]);
         }

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (INIT_MU0, INIT_SFLOOR, MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
+from .qp import (INIT_MU0, INIT_MU_MIN, INIT_Q_PER_VAR, INIT_SFLOOR, MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -171,6 +171,9 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
 
     u = np.clip(np.zeros(n), lb, ub) if boxed else np.zeros(n)
     mu0 = INIT_MU0 if init_mu0 is None else init_mu0
+    if mu0 > 0:
+        qrel = (1.0 / (INIT_Q_PER_VAR * n)) * np.abs(q).max()
+        mu0 = min(mu0, max(INIT_MU_MIN, qrel * qrel))
     sfl = INIT_SFLOOR if init_sfloor is None else init_sfloor
     s = np.maximum(w - sq.grow(sq.rollout(u)), sfl); z = mu0 / s if mu0 > 0 else np.ones(p)
     su = np.maximum(ub - u, sfl) if boxed else np.ones(n)
