@@ -45,7 +45,7 @@ constexpr double kPolishMu = 5e-5, kPolishRes = 3e-6;   // polish gate of the gr
 constexpr double kPolishDelta = 1e-10, kPolishTol = 1e-11;
 // initial point s = max(w - G u0, floor), z = mu0 / s, mu0 = clamp((|q|_inf / (kInitQPerVar n))^2, kInitMuMin, kInitMu0) (ipm_riccati.hip)
 constexpr double kInitMu0 = 100.0, kInitSFloor = 2.0, kInitMuMin = 1.0, kInitQPerVar = 3.5;
-constexpr int kPolishRefine = 3;
+constexpr int kPolishRefine = 2;
 constexpr int kPolishCorrections = 1;   // correction rounds of a rejected polish
 constexpr double kInf = std::numeric_limits<double>::infinity();
 

@@ -138,7 +138,8 @@ constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
 #define CARMPC_INIT_SFLOOR 2.0
 #endif
 constexpr double POLISH_DELTA = 1e-10;
-constexpr int POLISH_REFINE = 3;
+constexpr int POLISH_REFINE = 2;            // refinement passes of the polish solve (2: |u - u*| ~ 1e-10, same acceptances as 3)
+constexpr int POLISH_REFINE_CONSERVATIVE = 3;   // ... of the per-instance kernels, like the fallback kernels
 constexpr double POLISH_TOL = 1e-11;
 
 template <int N>
@@ -264,6 +265,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                                                                int32_t* __restrict__ iters_all, Settings S_all) {
     static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
     constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
+    constexpr int kPolRefine = HET ? POLISH_REFINE_CONSERVATIVE : POLISH_REFINE;
+    constexpr int kSolves = kPolRefine + 1 > 3 ? kPolRefine + 1 : 3;   // solves per trip: 3 of a step, kPolRefine + 1 of a polish
     constexpr double kMuMin = CARMPC_INIT_MU_MIN, kQInv = 1.0 / (CARMPC_INIT_Q_PER_VAR * 2 * N);
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
     constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;

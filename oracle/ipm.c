@@ -36,7 +36,7 @@
 #define INIT_Q_PER_VAR 3.5
 #define REFINE_MU 1e-6   /* refinement of the corrector only once mu <= REFINE_MU */
 #define POLISH_DELTA 1e-10
-#define POLISH_REFINE 3
+#define POLISH_REFINE 2   /* refinement passes of the polish solve; 3 in the fallback variant */
 #define POLISH_TOL 1e-11
 
 typedef struct {
@@ -116,9 +116,11 @@ static void gtmul(const qp_t* P, const double* y, double* out) { /* out = G' y *
 static int g_polish_corrections = 1;
 static double g_polish_mu = POLISH_MU, g_polish_res = POLISH_RES;
 static double g_init_mu0 = INIT_MU0, g_init_sfloor = INIT_SFLOOR;
-/* qp.FALLBACK_VARIANT = (0, 1e-6, 0, 0, 1): the single-attempt polish behind the conservative gate, z = 1
- * and slack floor 1 at the start */
-void oracle_set_variant(int corrections, double mu, double res, double init_mu0, double init_sfloor) {
+static int g_polish_refine = POLISH_REFINE;
+/* qp.FALLBACK_VARIANT = (0, 1e-6, 0, 0, 1, 3): the single-attempt polish (3 refinement passes) behind the
+ * conservative gate, z = 1 and slack floor 1 at the start */
+void oracle_set_variant(int corrections, double mu, double res, double init_mu0, double init_sfloor, int refine) {
+    g_polish_refine = refine;
     g_polish_corrections = corrections; g_polish_mu = mu; g_polish_res = res;
     g_init_mu0 = init_mu0; g_init_sfloor = init_sfloor;
 }
@@ -181,7 +183,7 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
         x[i] = 0.0; yu[i] = 0.0; yl[i] = 0.0;
     }
     for (int r = 0; r < p; ++r) yg[r] = 0.0;
-    for (int pass = 0; pass <= POLISH_REFINE; ++pass) {
+    for (int pass = 0; pass <= g_polish_refine; ++pass) {
         /* rx = -q - H x - A'y  (pass 0: x = y = 0) */
         for (int i = 0; i < n; ++i) {
             double v = -q[i];

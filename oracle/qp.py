@@ -48,9 +48,10 @@ INIT_Q_PER_VAR = 3.5       # (the best scale grows with the horizon: about 140 a
 INIT_SFLOOR = 2.0
 # the variant the fallback kernels (dense, staged, per-instance) run: z = 1 and slack floor 1 at the start,
 # one polish attempt behind the conservative gate
-FALLBACK_VARIANT = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0, init_mu0=0.0, init_sfloor=1.0)
+FALLBACK_VARIANT = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0, init_mu0=0.0, init_sfloor=1.0,
+                        polish_refine=3)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
-POLISH_REFINE = 3          # iterative-refinement passes of the polish
+POLISH_REFINE = 2          # iterative-refinement passes of the polish (2: |u - u*| ~ 1e-10, same acceptances as 3)
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
 POLISH_CORRECTIONS = 1     # correction rounds of a rejected polish (0: the single-attempt polish of the fallback kernels)
 UNBOXED_BOUND = 1e9        # |u_i| bound assumed by the Farkas test for unboxed variables
@@ -93,7 +94,7 @@ def opposite_pairs(G, w0, E):
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
         trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None,
-        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -153,7 +154,8 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         pmu = POLISH_MU if polish_mu is None else polish_mu
         if polish and rpn <= ptol * pscale and rdn <= ptol * dscale and mu <= pmu:
             up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
-                                 partner=partner, corrections=polish_corrections)
+                                 partner=partner, corrections=polish_corrections,
+                                 refine=POLISH_REFINE if polish_refine is None else polish_refine)
             if info is not None:
                 info.setdefault("polish", []).append((it, ok))
             if ok:
@@ -214,7 +216,8 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         su = su + a * dsu; zu = zu + a * dzu; sl = sl + a * dsl; zl = zl + a * dzl
     if polish:
         up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
-                             partner=partner)
+                             partner=partner, corrections=polish_corrections,
+                             refine=POLISH_REFINE if polish_refine is None else polish_refine)
         if ok:
             return up, STATUS_OPTIMAL, max_iter, z
     return u, STATUS_MAXITER, max_iter, z

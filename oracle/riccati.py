@@ -150,7 +150,7 @@ def _chol2_solve(L, b):
 
 
 def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None,
-        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None):
     """qp.ipm + qp.polish_step in stage form for one instance.  Returns (u, status, iters)."""
     x0 = np.asarray(x0, float)
     xref = np.asarray(xref, float)
@@ -218,7 +218,8 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
                 if lo - w @ z > 1e-12 * (np.abs(Gtz) @ bound_abs + np.abs(w) @ z):
                     return u, STATUS_INFEASIBLE, it
         if polish:
-            x, ok = _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, polish_corrections)
+            x, ok = _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, polish_corrections,
+                            POLISH_REFINE if polish_refine is None else polish_refine)
             if ok:
                 return x, STATUS_OPTIMAL, it
             polish_failed = True
@@ -269,7 +270,7 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
         it += 1
 
 
-def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=None):
+def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=None, refine=POLISH_REFINE):
     """qp.polish_step in stage form, with its correction rounds."""
     n = sq.n
     if corrections is None:
@@ -279,7 +280,7 @@ def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=Non
     al = sl < zl if boxed else np.zeros(n, bool)
     x = np.zeros(n)
     for attempt in range(corrections + 1):
-        x, ok, fix = _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat)
+        x, ok, fix = _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat, refine)
         if ok or fix is None or attempt == corrections:
             return x, ok
         nag, nau, nal = fix
@@ -289,7 +290,7 @@ def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=Non
     return x, False
 
 
-def _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat):
+def _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat, refine=POLISH_REFINE):
     """One polish on the active set (qp._polish_attempt in stage form)."""
     n = sq.n
     idl = 1.0 / POLISH_DELTA
@@ -299,7 +300,7 @@ def _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat):
     fac = sq.riccati_factor(dg, dbu + dbl)
     x = np.zeros(n); xv = np.zeros((sq.N + 1, 4))
     yg = np.zeros(sq.p); yu = np.zeros(n); yl = np.zeros(n)
-    for _ in range(POLISH_REFINE + 1):
+    for _ in range(refine + 1):
         gx = sq.grow(xv)
         ryg = np.where(ag, w - gx, 0.0)
         ryu = np.where(dbu > 0, ub - x, 0.0)
