@@ -11,7 +11,7 @@ Counting rules (/opt/skills/guides/MI355X_MICROARCH.md, HBM / rocprofv3 section)
   * FETCH_SIZE on gfx950 reports 1/2 of the bytes of wide coalesced reads -> doubled;
   * WRITE_SIZE taken as reported;
   * only the solve-kernel dispatches (name contains --match) are counted; one bench step
-    is one dispatch per environment segment, so bytes/step = total / (dispatches / segments).
+    is --segments consecutive dispatches; bytes/step = median over the steps of their sum.
 Updates profiles/traffic.json[key] with hbm_bytes_per_step (what bench.py reports as
 roofline.traffic)."""
 from __future__ import annotations
@@ -63,8 +63,17 @@ def main():
     nf, nw = len(fetch), len(write)
     if nf == 0 or nw == 0 or nf % a.segments or nw % a.segments:
         raise SystemExit(f"unexpected dispatch counts fetch={nf} write={nw}")
-    fetch_kb = sum(v["FETCH_SIZE"] for v in fetch.values()) / (nf // a.segments)
-    write_kb = sum(v["WRITE_SIZE"] for v in write.values()) / (nw // a.segments)
+    # bytes per step = median over the steps of the sum over the step's dispatches (a single dispatch now
+    # and then reports ten times its usual FETCH_SIZE; the median keeps such a glitch out, the per-dispatch
+    # values stay in the output)
+    def per_step(cnt, name):
+        ids = sorted(cnt)
+        steps = [sum(cnt[i][name] for i in ids[j:j + a.segments]) for j in range(0, len(ids), a.segments)]
+        steps.sort()
+        m = len(steps)
+        return steps[m // 2] if m % 2 else 0.5 * (steps[m // 2 - 1] + steps[m // 2])
+    fetch_kb = per_step(fetch, "FETCH_SIZE")
+    write_kb = per_step(write, "WRITE_SIZE")
     hbm = 2.0 * fetch_kb * 1024 + write_kb * 1024
     per = {}
     for d in a.counters:
