@@ -41,7 +41,8 @@ struct carmpc_cpu_problem {
 
 namespace {
 
-constexpr double kPolishMu = 5e-5, kPolishRes = 3e-6;   // polish gate of the grouped device kernel (ipm_riccati.hip)
+constexpr double kPolishMu = 1e-2, kPolishRes = 2e-4;   // polish gate of the grouped device kernel (ipm_riccati.hip)
+constexpr double kPolishAct = 0.003;                    // ... and its first active set: rows with s < kPolishAct z
 constexpr double kPolishDelta = 1e-10, kPolishTol = 1e-11;
 // initial point s = max(w - G u0, floor), z = mu0 / s, mu0 = clamp((|q|_inf / (kInitQPerVar n))^2, kInitMuMin, kInitMu0) (ipm_riccati.hip)
 constexpr double kInitMu0 = 100.0, kInitSFloor = 2.0, kInitMuMin = 1.0, kInitQPerVar = 3.5;
@@ -294,10 +295,10 @@ struct Solver {
     bool polish(const double* lbv, const double* ubv) {
         const double idl = 1.0 / kPolishDelta;
         const bool boxed = P.boxed;
-        for (int r = 0; r < p; ++r) d[r] = s[r] < z[r] ? idl : 0.0;
+        for (int r = 0; r < p; ++r) d[r] = s[r] < kPolishAct * z[r] ? idl : 0.0;
         for (int i = 0; i < n; ++i) {
-            dbu[i] = (boxed && su[i] < zu[i]) ? idl : 0.0;
-            dbl[i] = (boxed && sl[i] < zl[i]) ? idl : 0.0;
+            dbu[i] = (boxed && su[i] < kPolishAct * zu[i]) ? idl : 0.0;
+            dbl[i] = (boxed && sl[i] < kPolishAct * zl[i]) ? idl : 0.0;
         }
         for (int attempt = 0;; ++attempt) {
             if (polish_attempt(lbv, ubv, attempt < kPolishCorrections)) return true;

@@ -103,19 +103,27 @@ constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
 
 // The polish is attempted once mu <= POLISH_MU with both residuals within POLISH_RES (relative, like the
 // termination tolerance): far earlier than the IPM would terminate.  An accepted polish is the exact
-// optimum whenever it comes, so the gate only trades iterations saved (about 1.5 per instance against the
+// optimum whenever it comes, so the gate only trades iterations saved (about 3 per instance against the
 // conservative gate mu <= 1e-6, residuals within the termination tolerance) for more rejected attempts,
-// most of which the correction round repairs (measured: gates from 1e-6 / 1e-8 to 1e-3 / 1e-6, best
-// between 5e-5 / 3e-6 and 1e-4 / 3e-6 on every workload).  Overridable for such sweeps (tools/gpu/mkvar.sh).
+// most of which the correction round repairs (measured with the conservative first active set below: gates
+// from 5e-5 / 3e-6 to 2e-2 / 3e-4, best from 5e-3 / 1e-4 on; beyond 2e-2 the retry launch outgrows the
+// gain).  Overridable for such sweeps (tools/gpu/mkvar.sh).
 // The per-instance kernels keep the conservative gate, like the fallback kernels.
 #ifndef CARMPC_POLISH_MU
-#define CARMPC_POLISH_MU 5e-5
+#define CARMPC_POLISH_MU 1e-2
 #endif
 #ifndef CARMPC_POLISH_RES
-#define CARMPC_POLISH_RES 3e-6
+#define CARMPC_POLISH_RES 2e-4
 #endif
 constexpr double POLISH_MU = CARMPC_POLISH_MU, POLISH_RES = CARMPC_POLISH_RES;
 constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
+// First active set of a polish: the rows with s < POLISH_ACT z.  A conservative guess (few rows active, the
+// correction round adds the violated ones) is accepted far more often than s < z: 76 % instead of 50 % at
+// this gate, and 1.7 % instead of 13 % rejected after the correction (swept 0.001..30 for several gates).
+#ifndef CARMPC_POLISH_ACT
+#define CARMPC_POLISH_ACT 0.003
+#endif
+constexpr double POLISH_ACT = CARMPC_POLISH_ACT;
 // Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path z = mu0 / s with
 // mu0 = clamp((|q|_inf / (INIT_Q_PER_VAR n))^2, INIT_MU_MIN, INIT_MU0): a centred start whose distance from the
 // boundary follows the size of the linear term.  States far from the goal (large q, many active rows at the
@@ -266,6 +274,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
     constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
     constexpr int kPolRefine = HET ? POLISH_REFINE_CONSERVATIVE : POLISH_REFINE;
+    constexpr double kAct = HET ? 1.0 : POLISH_ACT;   // a row starts the polish active when s < kAct z
     constexpr int kSolves = kPolRefine + 1 > 3 ? kPolRefine + 1 : 3;   // solves per trip: 3 of a step, kPolRefine + 1 of a polish
     constexpr double kMuMin = CARMPC_INIT_MU_MIN, kQInv = 1.0 / (CARMPC_INIT_Q_PER_VAR * 2 * N);
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
@@ -1377,14 +1386,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     if (polish) {
                         // hand the instance to the polish launch: active rows (s < z) and active box rows
                         unsigned m = 0;
-                        for_used([&](const int s) __attribute__((always_inline)) { m |= (s_[s] < z_[s] ? 1u : 0u) << s; });
+                        for_used([&](const int s) __attribute__((always_inline)) { m |= (s_[s] < kAct * z_[s] ? 1u : 0u) << s; });
 #pragma unroll
                         for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
                             for (int c = 0; c < 2; ++c)
                                 if (own[sg] && boxed) {
-                                    m |= (BX(F_SU, sg, c) < BX(F_ZU, sg, c) ? 1u : 0u) << box_bit(sg, c, 0);
-                                    m |= (BX(F_SL, sg, c) < BX(F_ZL, sg, c) ? 1u : 0u) << box_bit(sg, c, 1);
+                                    m |= (BX(F_SU, sg, c) < kAct * BX(F_ZU, sg, c) ? 1u : 0u) << box_bit(sg, c, 0);
+                                    m |= (BX(F_SL, sg, c) < kAct * BX(F_ZL, sg, c) ? 1u : 0u) << box_bit(sg, c, 1);
                                 }
                         unsigned pos = 0;
                         if (j == 0) pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);

@@ -30,7 +30,7 @@ def load():
                                            dp, dp, ip, dp, ctypes.c_int64, dp, dp, dp, ip, ip,
                                            ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         lib.oracle_solve_batch.restype = ctypes.c_int
-        lib.oracle_set_variant.argtypes = [ctypes.c_int] + [ctypes.c_double] * 4 + [ctypes.c_int]
+        lib.oracle_set_variant.argtypes = [ctypes.c_int] + [ctypes.c_double] * 4 + [ctypes.c_int, ctypes.c_double]
         lib.oracle_set_variant.restype = None
         _lib = lib
     return _lib
@@ -59,11 +59,12 @@ class CpuProblem:
 
     def solve(self, x0, xref=None, tol=oq.TOL_RES, tol_mu=oq.TOL_MU, max_iter=oq.MAX_ITER, threads=0,
               polish_corrections=oq.POLISH_CORRECTIONS, polish_mu=oq.POLISH_MU, polish_res=oq.POLISH_RES,
-              init_mu0=oq.INIT_MU0, init_sfloor=oq.INIT_SFLOOR, polish_refine=oq.POLISH_REFINE):
+              init_mu0=oq.INIT_MU0, init_sfloor=oq.INIT_SFLOOR, polish_refine=oq.POLISH_REFINE,
+              polish_act=oq.POLISH_ACT):
         """``**oq.FALLBACK_VARIANT`` selects the algorithm variant of the fallback kernels."""
         lib = load()
         lib.oracle_set_variant(int(polish_corrections), float(polish_mu), float(polish_res), float(init_mu0),
-                               float(init_sfloor), int(polish_refine))
+                               float(init_sfloor), int(polish_refine), float(polish_act))
         x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, 4)
         B = x0.shape[0]
         xr = None if xref is None else np.ascontiguousarray(xref, dtype=np.float64).reshape(-1, 4)

@@ -28,8 +28,9 @@
 #define UNBOXED_BOUND 1e9
 #define PRE_TOL 1e-9
 #define STEP_FRAC 0.99
-#define POLISH_MU 5e-5    /* polish gate: mu <= POLISH_MU and residuals within max(POLISH_RES, tol) */
-#define POLISH_RES 3e-6
+#define POLISH_MU 1e-2    /* polish gate: mu <= POLISH_MU and residuals within max(POLISH_RES, tol) */
+#define POLISH_RES 2e-4
+#define POLISH_ACT 0.003  /* first active set of a polish: rows with s < POLISH_ACT z */
 #define INIT_MU0 100.0     /* initial point: s = max(w - G u0, INIT_SFLOOR), z = INIT_MU0 / s (qp.py) */
 #define INIT_SFLOOR 2.0
 #define INIT_MU_MIN 1.0     /* mu0 = clamp((|q|_inf / (INIT_Q_PER_VAR n))^2, INIT_MU_MIN, INIT_MU0) */
@@ -117,10 +118,12 @@ static int g_polish_corrections = 1;
 static double g_polish_mu = POLISH_MU, g_polish_res = POLISH_RES;
 static double g_init_mu0 = INIT_MU0, g_init_sfloor = INIT_SFLOOR;
 static int g_polish_refine = POLISH_REFINE;
-/* qp.FALLBACK_VARIANT = (0, 1e-6, 0, 0, 1, 3): the single-attempt polish (3 refinement passes) behind the
- * conservative gate, z = 1 and slack floor 1 at the start */
-void oracle_set_variant(int corrections, double mu, double res, double init_mu0, double init_sfloor, int refine) {
-    g_polish_refine = refine;
+static double g_polish_act = POLISH_ACT;
+/* qp.FALLBACK_VARIANT = (0, 1e-6, 0, 0, 1, 3, 1): the single-attempt polish (3 refinement passes, active set
+ * s < z) behind the conservative gate, z = 1 and slack floor 1 at the start */
+void oracle_set_variant(int corrections, double mu, double res, double init_mu0, double init_sfloor, int refine,
+                        double act) {
+    g_polish_refine = refine; g_polish_act = act;
     g_polish_corrections = corrections; g_polish_mu = mu; g_polish_res = res;
     g_init_mu0 = init_mu0; g_init_sfloor = init_sfloor;
 }
@@ -165,10 +168,10 @@ static int polish(const qp_t* P, const double* q, const double* w, work_t* W, do
     double* x = x_out;
     double ryu[64], ryl[64], dbox[64];
     if (n > 64) return 0;
-    for (int r = 0; r < p; ++r) dg[r] = W->s[r] < W->z[r] ? id : 0.0;
+    for (int r = 0; r < p; ++r) dg[r] = W->s[r] < g_polish_act * W->z[r] ? id : 0.0;
     for (int i = 0; i < n; ++i) {
-        dbu[i] = (boxed && W->su[i] < W->zu[i]) ? id : 0.0;
-        dbl[i] = (boxed && W->sl[i] < W->zl[i]) ? id : 0.0;
+        dbu[i] = (boxed && W->su[i] < g_polish_act * W->zu[i]) ? id : 0.0;
+        dbl[i] = (boxed && W->sl[i] < g_polish_act * W->zl[i]) ? id : 0.0;
     }
     /* attempt 0 on the active set of the iterate; correction rounds on the set the rejected
      * attempt names (oracle/qp.py::polish_step) */

@@ -33,8 +33,8 @@ MAX_ITER = 60
 STEP_FRAC = 0.99
 REFINE = 1                 # iterative-refinement passes on the corrector direction
 REFINE_MU = 1e-6           # ... only once mu <= REFINE_MU (D = z/s spans many decades)
-POLISH_MU = 5e-5           # attempt the active-set polish once mu <= POLISH_MU ...
-POLISH_RES = 3e-6          # ... and both residuals are within max(POLISH_RES, tol), relative.  An accepted
+POLISH_MU = 1e-2           # attempt the active-set polish once mu <= POLISH_MU ...
+POLISH_RES = 2e-4          # ... and both residuals are within max(POLISH_RES, tol), relative.  An accepted
 #                            polish is the exact optimum whenever it comes; the gate trades iterations for
 #                            rejected attempts (most are repaired by the correction round).
 # Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path, z = mu0 / s with
@@ -46,10 +46,13 @@ INIT_MU0 = 100.0
 INIT_MU_MIN = 1.0
 INIT_Q_PER_VAR = 3.5       # (the best scale grows with the horizon: about 140 at N = 20, 70 at N = 10, 35 at N = 5)
 INIT_SFLOOR = 2.0
+# First active set of a polish: the rows with s < POLISH_ACT z -- a conservative guess (few rows, the correction
+# round adds the violated ones) is accepted far more often than s < z.
+POLISH_ACT = 0.003
 # the variant the fallback kernels (dense, staged, per-instance) run: z = 1 and slack floor 1 at the start,
 # one polish attempt behind the conservative gate
 FALLBACK_VARIANT = dict(polish_corrections=0, polish_mu=1e-6, polish_res=0.0, init_mu0=0.0, init_sfloor=1.0,
-                        polish_refine=3)
+                        polish_refine=3, polish_act=1.0)
 POLISH_DELTA = 1e-10        # regularisation of the polish KKT system
 POLISH_REFINE = 2          # iterative-refinement passes of the polish (2: |u - u*| ~ 1e-10, same acceptances as 3)
 POLISH_TOL = 1e-11         # acceptance: primal violation and negative multipliers, relative
@@ -94,7 +97,7 @@ def opposite_pairs(G, w0, E):
 
 def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER,
         trace=None, refine=REFINE, polish=True, info=None, partner=None, polish_corrections=None,
-        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None, polish_act=None):
     """Dense Mehrotra IPM for  min 1/2 u'Hu + q'u  s.t. G u <= w, lb <= u <= ub.
 
     G rows must be normalised (``normalize_rows``).  lb/ub None => no box.
@@ -155,7 +158,7 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
         if polish and rpn <= ptol * pscale and rdn <= ptol * dscale and mu <= pmu:
             up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
                                  partner=partner, corrections=polish_corrections,
-                                 refine=POLISH_REFINE if polish_refine is None else polish_refine)
+                                 refine=POLISH_REFINE if polish_refine is None else polish_refine, act=polish_act)
             if info is not None:
                 info.setdefault("polish", []).append((it, ok))
             if ok:
@@ -217,14 +220,14 @@ def ipm(H, q, G, w, lb=None, ub=None, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_I
     if polish:
         up, ok = polish_step(H, q, G, w, lb if boxed else None, ub if boxed else None, s, z, su, zu, sl, zl,
                              partner=partner, corrections=polish_corrections,
-                             refine=POLISH_REFINE if polish_refine is None else polish_refine)
+                             refine=POLISH_REFINE if polish_refine is None else polish_refine, act=polish_act)
         if ok:
             return up, STATUS_OPTIMAL, max_iter, z
     return u, STATUS_MAXITER, max_iter, z
 
 
 def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, refine=POLISH_REFINE,
-                partner=None, corrections=None):
+                partner=None, corrections=None, act=None):
     """Active-set polish.  Active set from the IPM iterate (s < z); solve the
     equality-constrained KKT [[H, A'], [A, 0]] [x; y] = [-q; b_act] by iterative refinement on
     the regularised factor  H + A'A/delta  (the IPM's M with d = 1/delta on active rows, 0 else);
@@ -240,9 +243,10 @@ def polish_step(H, q, G, w, lb, ub, s, z, su, zu, sl, zl, delta=POLISH_DELTA, re
     boxed = lb is not None
     if corrections is None:
         corrections = POLISH_CORRECTIONS
-    ag = s < z
-    au = su < zu if boxed else np.zeros(n, bool)
-    al = sl < zl if boxed else np.zeros(n, bool)
+    act = POLISH_ACT if act is None else act
+    ag = s < act * z
+    au = su < act * zu if boxed else np.zeros(n, bool)
+    al = sl < act * zl if boxed else np.zeros(n, bool)
     x = np.zeros(n)
     for attempt in range(corrections + 1):
         x, ok, fix = _polish_attempt(H, q, G, w, lb, ub, ag, au, al, delta, refine, partner)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .qp import (INIT_MU0, INIT_MU_MIN, INIT_Q_PER_VAR, INIT_SFLOOR, MAX_ITER, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
+from .qp import (INIT_MU0, INIT_MU_MIN, INIT_Q_PER_VAR, INIT_SFLOOR, MAX_ITER, POLISH_ACT, POLISH_CORRECTIONS, POLISH_DELTA, POLISH_MU, POLISH_RES, POLISH_REFINE, POLISH_TOL, PRE_TOL, REFINE_MU, STEP_FRAC,
                  STATUS_INFEASIBLE, STATUS_MAXITER, STATUS_NUMERICAL, STATUS_OPTIMAL, TOL_MU, TOL_RES,
                  UNBOXED_BOUND, ZERO_ROW, _maxstep, opposite_pairs)
 
@@ -150,7 +150,7 @@ def _chol2_solve(L, b):
 
 
 def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, polish_corrections=None,
-        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None):
+        polish_mu=None, polish_res=None, init_mu0=None, init_sfloor=None, polish_refine=None, polish_act=None):
     """qp.ipm + qp.polish_step in stage form for one instance.  Returns (u, status, iters)."""
     x0 = np.asarray(x0, float)
     xref = np.asarray(xref, float)
@@ -219,7 +219,8 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
                     return u, STATUS_INFEASIBLE, it
         if polish:
             x, ok = _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, polish_corrections,
-                            POLISH_REFINE if polish_refine is None else polish_refine)
+                            POLISH_REFINE if polish_refine is None else polish_refine,
+                            POLISH_ACT if polish_act is None else polish_act)
             if ok:
                 return x, STATUS_OPTIMAL, it
             polish_failed = True
@@ -270,14 +271,15 @@ def ipm(sq: StageQP, x0, xref, tol=TOL_RES, tol_mu=TOL_MU, max_iter=MAX_ITER, po
         it += 1
 
 
-def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=None, refine=POLISH_REFINE):
+def _polish(sq, q, w, lb, ub, boxed, s, z, su, zu, sl, zl, Rhat, corrections=None, refine=POLISH_REFINE,
+            act=POLISH_ACT):
     """qp.polish_step in stage form, with its correction rounds."""
     n = sq.n
     if corrections is None:
         corrections = POLISH_CORRECTIONS
-    ag = s < z
-    au = su < zu if boxed else np.zeros(n, bool)
-    al = sl < zl if boxed else np.zeros(n, bool)
+    ag = s < act * z
+    au = su < act * zu if boxed else np.zeros(n, bool)
+    al = sl < act * zl if boxed else np.zeros(n, bool)
     x = np.zeros(n)
     for attempt in range(corrections + 1):
         x, ok, fix = _polish_attempt(sq, q, w, lb, ub, boxed, ag, au, al, Rhat, refine)

@@ -118,7 +118,7 @@ def test_cpu_path_iteration_limit():
     asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
     X = _x0(np.random.default_rng(5), asm.goal[0], 512)
     qp = _cpu_qp(asm)
-    for mi in (5, 7):
+    for mi in (2, 4):
         uc, sc, ic = CpuProblem(asm).solve(X, max_iter=mi, threads=4)
         u, st, it = qp.solve(X, settings=SolverSettings(max_iter=mi), threads=4)
         np.testing.assert_array_equal(st, sc)

@@ -202,7 +202,7 @@ def test_iteration_limit(gpu_available, kernel):
     asm, qp = _setup("RoadMultipleCarsEnv", 20)
     X = _random_x0(np.random.default_rng(5), asm.goal[0], 2048)
     cp = CpuProblem(asm)
-    for mi in (5, 7):
+    for mi in (3, 5):
         uc, sc, ic = cp.solve(X, max_iter=mi, **({} if kernel == 7 else oq.FALLBACK_VARIANT))
         assert (sc == 2).sum() > 200 and (sc == 0).sum() > 100
         u, st, it = qp.solve(torch.as_tensor(X).cuda(), settings=SolverSettings(max_iter=mi, kernel=kernel))
