@@ -298,7 +298,7 @@ struct RicWork {
     int32_t round;        // pipeline round of this launch
 };
 // One round of (iterations, polish): a second one for the instances whose polish was rejected measured
-// slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 1.5 % with the
+// slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 2-3 % with the
 // correction round and the early polish gate) -- it solves them with the lean kernels but still leaves a
 // latency-bound single-kernel tail for the ones rejected again.
 constexpr int kRicRounds = 1;

@@ -1523,7 +1523,7 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
     W.retry_idx = reinterpret_cast<int32_t*>(W.pend_rec + (size_t)kRicRecWords * n);
     e = launch_zero_u32(W.cnt, (int)ncnt, stream);
     // rounds of (iterations, polish): round r takes the instances whose first r polishes were rejected
-    // (one or two per cent after round 0); what is left after the last round goes to the single kernel
+    // (two or three per cent after round 0); what is left after the last round goes to the single kernel
     for (W.round = 0; W.round < kRicRounds && e == hipSuccess; ++W.round) {
         e = ric_dispatch<false, 1>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
         if (e == hipSuccess) e = ric_dispatch<false, 2>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
