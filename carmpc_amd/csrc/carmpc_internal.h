@@ -303,7 +303,7 @@ struct RicWork {
 // latency-bound single-kernel tail for the ones rejected again.
 constexpr int kRicRounds = 1;
 // smallest batch (instances of one call) solved by the pipeline: measured cross-over between 32,768 (single
-// kernel 10.1M QP/s, pipeline 10.0M) and 65,536 (10.6M, 11.5M) on RoadOneCarEnv, N = 20
+// kernel 14.3M QP/s, pipeline 14.4M) and 65,536 (14.9M, 16.7M) on RoadOneCarEnv, N = 20
 constexpr int kRicPipelineMin = 49152;
 static_assert(4 * kRicRounds < kRicClaimStride, "counter slots per segment");
 hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double* xref, double* u_out, int64_t ld_u,
