@@ -87,7 +87,8 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise CarMPCNativeError(f"{LIB_PATH} not found: build it with `python -m carmpc_amd.build` "
-                                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+                                "(hipcc --offload-arch=gfx950); the GPU kernels and the host path "
+                                "(carmpc_cpu_*) both live in that library, nothing runs without it")
     lib = ctypes.CDLL(LIB_PATH)
     vp, dp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
     i32, i64 = ctypes.c_int32, ctypes.c_int64

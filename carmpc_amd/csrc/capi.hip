@@ -811,6 +811,8 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
     for (int j = 0; j < nprobs; ++j) {
         const int64_t b0 = offsets[j], b1 = offsets[j + 1];
         if (b0 < 0 || b1 < b0) return fail(CARMPC_EINVAL, "offsets must be non-negative and non-decreasing");
+        // (32-bit claim counters and int32 rows in the work lists, as in carmpc_solve_batch)
+        if (b1 - offsets[0] > INT32_MAX) return fail(CARMPC_EUNSUPPORTED, "segments exceed 2^31 - 1 instances");
         if (b1 == b0) continue;
         if (!probs[j]) return fail(CARMPC_EINVAL, "null problem in segment list");
         if (ld_u < probs[j]->dev.n) return fail(CARMPC_EINVAL, "ld_u smaller than n");
@@ -1229,6 +1231,8 @@ int solve_batch_with_claim(const carmpc_problem* P, int64_t batch, const double*
     if (!P) return fail(CARMPC_EINVAL, "null problem");
     if (batch < 0) return fail(CARMPC_EINVAL, "negative batch");
     if (batch == 0) return CARMPC_OK;
+    // the kernels count instances in 32-bit claim counters and keep rows as int32 in their work lists
+    if (batch > INT32_MAX) return fail(CARMPC_EUNSUPPORTED, "batch exceeds 2^31 - 1 instances");
     if (!x0 || !u_out || !status) return fail(CARMPC_EINVAL, "null batch pointer");
     Settings s = make_settings(settings);
     s.claim = claim;

@@ -407,8 +407,9 @@ __global__ void het_split_kernel(int64_t batch, const int32_t* ok, int32_t* idx_
 hipError_t launch_het_split(int64_t batch, const int32_t* ok, int32_t* idx_ok, int32_t* cnt_ok, int32_t* idx_bad,
                             int32_t* cnt_bad, hipStream_t s) {
     if (batch <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(cnt_ok, 0, sizeof(int32_t), s);
-    if (e == hipSuccess) e = hipMemsetAsync(cnt_bad, 0, sizeof(int32_t), s);
+    // cleared by the fill kernel, like every counter of the library (a caller may capture the launches)
+    hipError_t e = launch_zero_u32(reinterpret_cast<unsigned*>(cnt_ok), 1, s);
+    if (e == hipSuccess) e = launch_zero_u32(reinterpret_cast<unsigned*>(cnt_bad), 1, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(het_split_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, s, batch, ok, idx_ok,
                        cnt_ok, idx_bad, cnt_bad);

@@ -292,6 +292,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     const int seg = nseg > 1 ? (home + kseg_i) % nseg : 0;
     const DevProblem& P = T.P[seg];
     const int64_t seg0 = T.off[seg], batch = T.off[seg + 1] - seg0;
+    const int64_t lst0 = seg0 - T.off[0];   // the segment's start in the work lists, which begin at the run's first instance
     const double* __restrict__ x0 = x0_all + seg0 * NX;
     const double* __restrict__ xref = xref_all ? xref_all + seg0 * NX : nullptr;
     double* __restrict__ u_out = u_all + seg0 * ld_u;
@@ -304,7 +305,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             if (W.round == 0) {
                 S.claim = wc + 0;
             } else {   // the previous round's rejected polishes
-                S.index = W.retry_idx + seg0;
+                S.index = W.retry_idx + lst0;
                 S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
                 S.claim = wc + 4 * W.round;
             }
@@ -313,7 +314,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round + 1);
             S.claim = wc + 4 * W.round + 2;
         } else {   // after the last round
-            S.index = W.retry_idx + seg0;
+            S.index = W.retry_idx + lst0;
             S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
             S.claim = wc + 4 * W.round;
         }
@@ -997,7 +998,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     bool live = slot < nlive;   // the group has an instance to work on
     // slot -> row: the caller's list, the hand-off record (polish launch), or the slot itself
     auto row_of = [&](int64_t sl, bool lv) -> int64_t {
-        if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(seg0 + sl) * kRicRecWords + kRicRecRow] : sl;
+        if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(lst0 + sl) * kRicRecWords + kRicRecRow] : sl;
         else return lv && S.index ? (int64_t)S.index[sl] : sl;
     };
     int64_t inst = row_of(slot, live);
@@ -1067,7 +1068,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 #pragma unroll
             for (int k = 0; k < NX; ++k) {
                 if constexpr (MODE == 2)
-                    xv0[k] = reinterpret_cast<const double*>(W.pend_rec + (seg0 + slot) * kRicRecWords + kRicRecX0)[k];
+                    xv0[k] = reinterpret_cast<const double*>(W.pend_rec + (lst0 + slot) * kRicRecWords + kRicRecX0)[k];
                 else
                     xv0[k] = x0[inst * NX + k];
                 xr[k] = xref ? xref[inst * NX + k] : Igoal[k];
@@ -1398,7 +1399,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         unsigned pos = 0;
                         if (j == 0) pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);
                         pos = __shfl(pos, lane & ~(G16 - 1), 64);
-                        uint32_t* hrec = W.pend_rec + (seg0 + pos) * kRicRecWords;
+                        uint32_t* hrec = W.pend_rec + (lst0 + pos) * kRicRecWords;
                         hrec[j] = m;
                         if (j < NX) reinterpret_cast<double*>(hrec + kRicRecX0)[j] = x0[inst * NX + j];
                         if (j == 0) {
@@ -1416,7 +1417,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 // the hand-off record replaces residuals and decisions
                 polish = true;
                 if (active && !RIC_REPOL) {
-                    const uint32_t* hrec = W.pend_rec + (seg0 + slot) * kRicRecWords;
+                    const uint32_t* hrec = W.pend_rec + (lst0 + slot) * kRicRecWords;
                     actm = hrec[j];
                     it = (int)hrec[kRicRecIt];
                 }
@@ -1536,10 +1537,14 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
 // no-allocation entry) get the single kernel, and so do small batches: the pipeline's last launch has
 // the latency of one complete solve however few instances it holds.
 bool ric_wants_pipeline(const Settings& s, int64_t total) {
+#ifdef CARMPC_RIC_PIPELINE_MIN_ENV   // experiment builds only (tools/gpu/pipe_threshold.sh): threshold from the environment
     static const long long min_total = [] {
-        const char* v = getenv("CARMPC_RIC_PIPELINE_MIN");   // experiment switch
+        const char* v = getenv("CARMPC_RIC_PIPELINE_MIN");
         return v ? atoll(v) : (long long)kRicPipelineMin;
     }();
+#else
+    constexpr long long min_total = kRicPipelineMin;
+#endif
     return !s.index && !s.count && !s.claim && total >= min_total;
 }
 }  // namespace

@@ -105,3 +105,45 @@ def test_empty_segments(gpu_available):
     u2, st2, _ = probs[1].solve(X)
     torch.cuda.synchronize()
     assert torch.equal(st, st2) and torch.equal(u[:, :probs[1].n], u2)
+
+
+@pytest.mark.parametrize("case", ["first_offset_positive", "leading_other_horizon", "six_segments"])
+def test_pipeline_runs_that_do_not_start_at_instance_zero(gpu_available, case):
+    """Runs of segments large enough for the three-launch form (49,152 instances and more) whose first
+    instance is not row 0 of the call: a positive first offset, a run behind a segment of another
+    horizon, and the second run of a call with more segments than one launch carries.  The hand-off
+    and retry lists of such a run begin at the run's first instance."""
+    import torch
+    from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.mpc import MPCStateFB
+    from carmpc_amd.qp import solve_segments
+    p20 = _problems()
+    if case == "first_offset_positive":
+        probs, offsets = [p20[1], p20[2]], np.array([5000, 33000, 61000])
+    elif case == "leading_other_horizon":
+        p10 = MPCStateFB(dt=DT_CONTROL, N=10, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT,
+                         env=ENVIRONMENTS["RoadEnv"](), terminal_set_dir=TERMINAL_SETS).qp
+        probs, offsets = [p10, p20[0], p20[2]], np.array([0, 3000, 30000, 56000])
+    else:
+        probs = [p20[0], p20[1], p20[2], p20[0], p20[1], p20[2]]
+        offsets = np.concatenate([[0], np.cumsum([2500, 2500, 2500, 2500, 26000, 26000])])
+    B = int(offsets[-1]) + 100                     # rows beyond the last offset belong to no segment
+    X = torch.as_tensor(_states(B, 21)).cuda()
+    u = torch.full((B, 40), -7.0, dtype=torch.float64, device="cuda")
+    st = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+    it = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+    solve_segments(probs, offsets, X, out=(u, st, it))
+    torch.cuda.synchronize()
+    outside = np.ones(B, bool)
+    outside[int(offsets[0]):int(offsets[-1])] = False
+    outside = torch.as_tensor(outside).cuda()
+    assert bool((st[outside] == -7).all()) and bool((u[outside] == -7.0).all())     # nothing written outside the segments
+    for j, p in enumerate(probs):
+        sl = slice(int(offsets[j]), int(offsets[j + 1]))
+        u1, s1, i1 = p.solve(X[sl])
+        torch.cuda.synchronize()
+        assert torch.equal(s1, st[sl]) and torch.equal(i1, it[sl])
+        ok = s1 == 0
+        assert int(ok.sum()) > 0
+        assert float((u1[ok] - u[sl, :p.n][ok]).abs().max()) <= 1e-12

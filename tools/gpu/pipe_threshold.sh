@@ -1,5 +1,7 @@
 #!/bin/bash
-# pipeline vs single kernel by batch size (CARMPC_RIC_PIPELINE_MIN: 0 = always pipeline, huge = never)
+# pipeline vs single kernel by batch size (CARMPC_RIC_PIPELINE_MIN: 0 = always pipeline, huge = never).
+# Needs an experiment build that reads the variable:
+#   bash tools/gpu/mkvar.sh pmin -DCARMPC_RIC_PIPELINE_MIN_ENV ; CARMPC_LIB=build/exp_pmin/libcarmpc.so
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for B in 2048 8192 16384 32768 65536 131072; do
