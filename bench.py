@@ -159,7 +159,12 @@ class GpuBackend:
         import torch
         self.torch = torch
         ndev = torch.cuda.device_count()
-        if local_rank >= ndev > 0:      # more ranks than GPUs (a rehearsal of the N>1 flow on one GPU): share
+        self.gpus_visible = ndev
+        if local_rank >= ndev > 0:      # more ranks than GPUs: only as an explicit rehearsal of the N>1 flow
+            if not args.share_gpus:
+                raise SystemExit(f"bench: local rank {local_rank} has no GPU of its own ({ndev} visible); a run whose "
+                                 "ranks share GPUs measures no scaling (--share-gpus runs it as a rehearsal and "
+                                 "marks the line)")
             print(f"bench: local rank {local_rank} shares GPU {local_rank % ndev} ({ndev} visible): "
                   "throughput of this run is not a scaling number", file=sys.stderr)
             local_rank %= ndev
@@ -250,6 +255,8 @@ class CpuBackend:
     """The library's CPU QP path (carmpc_cpu_solve_batch) under the same control flow."""
     name = "cpu"
 
+    gpus_visible = None
+
     def __init__(self, args, local_rank):
         self.args = args
         self.device = "cpu"
@@ -304,6 +311,11 @@ def run(args, backend_cls=None) -> dict | None:
     """The benchmark's control flow; returns the result line on rank 0 (None elsewhere).
     ``backend_cls`` is injectable so the distributed flow can run anywhere."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # one rank per GPU: a line that says n_gpus = N must come from N ranks
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE is {world}: launch one rank per GPU "
+                         f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}), "
+                         "or run bench.py --gpus N without a launcher and it starts the ranks itself")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -380,6 +392,13 @@ def run(args, backend_cls=None) -> dict | None:
     }
     if e2e is not None:
         out["e2e_qps_pcie_inclusive"] = round(e2e * world, 1)
+    gpus_visible = getattr(be, "gpus_visible", None)
+    if gpus_visible is not None:
+        out["gpus_visible"] = gpus_visible
+        out["ranks_share_gpu"] = world > gpus_visible
+        if out["ranks_share_gpu"]:
+            out["note"] = "REHEARSAL: ranks shared GPUs (--share-gpus); value is not a scaling measurement"
+    assert out["n_gpus"] == args.gpus
 
     # CPU baseline and I_ref: the oracle on a bounded sample of rank 0's shard
     seg = np.diff(offsets)
@@ -471,11 +490,44 @@ def parse_args(argv=None):
                     help="one carmpc_solve_batch launch per environment instead of one carmpc_solve_segments call")
     ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 7 riccati)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="allow more ranks than visible GPUs (rehearsal of the N>1 flow; the line is marked)")
     return ap.parse_args(argv)
 
 
+def spawn_ranks(args, argv) -> int:
+    """``bench.py --gpus N`` from a plain shell (no launcher, WORLD_SIZE unset): start N ranks of this
+    script as fresh child processes, one per GPU, before this process has touched the GPU, and
+    relay rank 0's line.  Returns the exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    line, _ = procs[0].communicate()
+    codes = [p.wait() for p in procs]
+    if any(codes):
+        print(f"bench: rank exit codes {codes}", file=sys.stderr)
+        return next(c for c in codes if c) or 1
+    for ln in line.splitlines():      # (gloo prints its own connection notes on stdout: keep stdout to the result)
+        print(ln, file=sys.stdout if ln.startswith("{") else sys.stderr, flush=True)
+    return 0
+
+
 def main(argv=None):
-    out = run(parse_args(argv))
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be at least 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, argv))
+    out = run(args)
     if out is not None:
         print(json.dumps(out), flush=True)
 

@@ -77,3 +77,37 @@ def test_bench_single_rank_config4_flow_on_cpu():
                                       "--per-gpu", "96", "--cpu-threads", "2", "--cpu-sample", "48"]))
     assert out["config"]["workload"].startswith("config4") and out["config"]["step"].startswith("observer")
     assert sum(out["status_split"].values()) == 96 and out["status_split"]["optimal"] > 10
+
+
+def _plain_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def test_bench_starts_its_own_ranks_from_a_plain_shell():
+    """`python bench.py --gpus 2` without a launcher: the script starts two ranks itself and relays
+    rank 0's line, so the line's n_gpus is the number of ranks that ran."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "cpu", "--steps", "1",
+                        "--warmup", "0", "--per-gpu", "120", "--cpu-threads", "2", "--no-cpu"],
+                       env=_plain_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 240 and out["config"]["parallelism"].startswith("shard2")
+
+
+def test_bench_refuses_a_world_size_that_differs_from_gpus():
+    """A launcher that starts one rank while the command line says --gpus 2 (or the reverse) must not
+    produce a line."""
+    import subprocess
+    import sys
+    env = _plain_env()
+    env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "cpu", "--steps", "1",
+                        "--warmup", "0", "--per-gpu", "60", "--no-cpu"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and r.stdout.strip() == "" and "WORLD_SIZE" in r.stderr
