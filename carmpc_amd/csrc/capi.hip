@@ -605,6 +605,7 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
     auto* P = new carmpc_problem();
     P->device = dev;
+    noalloc_prepare_device(dev);   // (resolves the no-allocation entry's scratch address now: that entry may first run under graph capture)
     P->assembled = true;
     const int nt = d->n_term_rows, ns = d->n_state_rows;
     const int p_all = nt + ns * N;
@@ -731,6 +732,7 @@ int carmpc_problem_create_dense(int32_t n, int32_t p, int32_t nx, const double* 
     classify(nrm, qp, pre);
     auto* P = new carmpc_problem();
     HIP_TRY(hipGetDevice(&P->device), "hipGetDevice");
+    noalloc_prepare_device(P->device);
     DevProblem& D = P->dev;
     D.n = n; D.nv = nv; D.p = (int)qp.size(); D.npre = (int)pre.size(); D.ldg = nv + 2; D.N = 0; D.nu = 0;
     size_t lds = 0;

@@ -152,6 +152,9 @@ int solve_batch_with_claim(const carmpc_problem* P, int64_t batch, const double*
                            int32_t* status, int32_t* iters, const carmpc_settings* settings, unsigned* claim,
                            hipStream_t stream);
 int problem_device(const carmpc_problem* P);
+// noalloc.hip: resolve the device address of the static scratch of GPU `dev` (current device) once; problem
+// creation calls it, so that carmpc_solve_batch_noalloc itself makes no symbol lookup on that GPU any more
+int noalloc_prepare_device(int dev);
 int set_error(int code, const char* msg);   // records the calling thread's last-error message, returns code
 
 // Argument blocks of the setup kernels (assembly.hip).

@@ -1469,10 +1469,15 @@ bool riccati_supported_N(int N) { return N == 10 || N == 20; }
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
-template <class Kern>
+// Wavefronts per workgroup by horizon: one workgroup per CU, so this is the number of waves that share a
+// CU's four SIMDs.  What limits it is LDS (the per-wave record, row and input state below).
+#ifndef CARMPC_RIC_WPB10
+#define CARMPC_RIC_WPB10 4
+#endif
+constexpr int ric_wpb(int N) { return N <= 10 ? CARMPC_RIC_WPB10 : 4; }
+template <int WPB, class Kern>
 hipError_t ric_launch(Kern kern, const RicSegs& T, const RicWork& W, int64_t total, const double* x0, const double* xref,
                       double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
-    constexpr int WPB = 4;
     int dev = 0, cus = 0, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -1491,14 +1496,13 @@ template <bool HET, int MODE>
 hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const double* x0, const double* xref,
                         double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
-    constexpr int WPB = 4;
     const bool bike = T.P[0].ric == 2;
     if (HET && !bike) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
 #define RIC_GO(NN, MODEL) \
-    ric_launch(ipm_riccati_kernel<NN, WPB, MODEL, HET, MODE>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
+    ric_launch<ric_wpb(NN)>(ipm_riccati_kernel<NN, ric_wpb(NN), MODEL, HET, MODE>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
     switch (T.P[0].N) {
         case 10: return bike ? RIC_GO(10, BicycleModel) : RIC_GO(10, DenseModel);
         case 20: return bike ? RIC_GO(20, BicycleModel) : RIC_GO(20, DenseModel);

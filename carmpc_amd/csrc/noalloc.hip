@@ -21,7 +21,8 @@ static __device__ __align__(256) unsigned scratch[64];
 
 namespace {
 // Device address of `scratch` on each GPU (every GPU has its own copy at its own address),
-// resolved on the first call made with that device current.
+// resolved once per device with that device current: when a problem is created on it
+// (noalloc_prepare_device), else on the first call of the entry point.
 int scratch_address(int dev, unsigned** out) {
     static std::mutex mu;
     static unsigned* ptr[64] = {};
@@ -38,6 +39,11 @@ int scratch_address(int dev, unsigned** out) {
     return CARMPC_OK;
 }
 }  // namespace
+
+int carmpc::noalloc_prepare_device(int dev) {
+    unsigned* p = nullptr;
+    return scratch_address(dev, &p);
+}
 
 extern "C" int carmpc_solve_batch_noalloc(const carmpc_problem* P, int64_t batch, const double* x0, const double* xref,
                                           double* u_out, int32_t* status, int32_t* iters,

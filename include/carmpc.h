@@ -155,7 +155,10 @@ int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* 
  * allocation, and the call makes no hipMalloc, hipFree or other allocating call.  batch <= CARMPC_NOALLOC_MAX_BATCH, else CARMPC_EUNSUPPORTED.
  * All calls on one GPU share that array: the counter is cleared at the start of each call (on
  * `stream`), and two calls whose kernels overlap on one GPU -- from different streams or threads --
- * race on it.  Call it with the problem's device current. */
+ * race on it.  Call it with the problem's device current.  The array's device address is looked up
+ * when a problem is created on the GPU, so the call may be the first thing a capturing stream
+ * records; a captured call replays like any kernel sequence (the counter is cleared by a small
+ * fill kernel, not a memset node). */
 #define CARMPC_NOALLOC_MAX_BATCH ((int64_t)1 << 30)
 int carmpc_solve_batch_noalloc(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
                                double* u_out, int32_t* status, int32_t* iters,

@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from conftest import CONFIGS, GOLDEN, REPO, TERMINAL_SETS
+from costs import OBJ_RTOL, objective, objective_gap, stage_cost, terminal_cost
 
 from oracle import assembly as oa
 from oracle import qp as oq
@@ -46,7 +47,8 @@ def test_cpu_path_golden_vectors(name, N):
     ok = st == 0
     assert np.abs(u[ok] - g["u_star"][ok]).max() <= U_TOL
     assert np.abs(it[ok] - g["iters"][ok]).max() <= 1          # same algorithm as the oracle
-    for x0, uu in zip(g["x0"][ok], u[ok]):
+    for x0, uu, us in zip(g["x0"][ok], u[ok], g["u_star"][ok]):
+        assert objective_gap(asm, x0, uu, us) <= OBJ_RTOL
         w = asm.w0 - asm.E @ x0
         assert (asm.G @ uu - w).max() <= VIOL_TOL and (uu - asm.ub).max() <= VIOL_TOL and (asm.lb - uu).max() <= VIOL_TOL
         xN = (asm.T @ x0 + asm.S @ uu)[-4:]
@@ -177,6 +179,26 @@ def test_config1_statefb_loop_on_cpu_matches_golden_trace():
     assert step + 1 == len(g["states"]) == 152
 
 
+@pytest.mark.parametrize("name,N", [("RoadEnv", 10), ("RoadMultipleCarsEnv", 20)])
+def test_statefb_step_side_effects_on_cpu(name, N):
+    """MPCStateFB.step's side-effect attributes (mpc.py:341-347) against the reference formulas
+    evaluated at the golden optimum: x_horizon, u_horizon, terminal_cost (absolute x_N), stage_cost."""
+    from carmpc_amd.environments import ENVIRONMENTS
+    from carmpc_amd.mpc import MPCStateFB
+    asm = oa.build(name, N, terminal_set_dir=TERMINAL_SETS)
+    g = np.load(os.path.join(GOLDEN, f"qp_{name}_N{N}.npz"))
+    c = MPCStateFB(0.2, N, [0, 0, 0, 3], [0, 0], env=ENVIRONMENTS[name](), terminal_set_dir=TERMINAL_SETS, device="cpu")
+    for i in np.where(g["status"] == 0)[0][:6]:
+        x0, us = g["x0"][i], g["u_star"][i]
+        u0 = c.step(x0)
+        np.testing.assert_allclose(u0, us[:2], rtol=0, atol=U_TOL)
+        np.testing.assert_allclose(c.u_horizon, us.reshape(-1, 2), rtol=0, atol=U_TOL)
+        np.testing.assert_allclose(c.x_horizon, (asm.T @ x0 + asm.S @ us).reshape(-1, 4), rtol=0, atol=1e-6)
+        tc, sc = terminal_cost(asm, x0, us), stage_cost(asm, x0, us, oa.STAGE_COST_Q, oa.STAGE_COST_R)
+        assert abs(c.terminal_cost - tc) <= 1e-7 * max(1.0, abs(tc))
+        assert abs(c.stage_cost - sc) <= 1e-7 * max(1.0, abs(sc))
+
+
 def test_outputfb_and_disturbance_controllers_on_cpu():
     """MPCOutputFB.step (mpc.py:450-492) and MPCOutputFBWithDisturbance.step (mpc.py:614-667) with
     the host observer forms and the CPU QP, against the oracle step by step."""
@@ -198,6 +220,8 @@ def test_outputfb_and_disturbance_controllers_on_cpu():
         u = c.step(sim.output)
         assert r["status"] == 0 and np.abs(u - r["u_exact"][:2]).max() <= U_TOL
         np.testing.assert_allclose(c.x_estimate, xhat, rtol=0, atol=1e-9)
+        j_ref = objective(asm, xhat, r["u_exact"], asm.goal)                 # MPCOutputFB.cost (mpc.py:478, 487)
+        assert abs(c.cost - j_ref) <= OBJ_RTOL * max(1.0, abs(j_ref))
         u = r["u_exact"][:2]
         c.previous_u = u.copy()
     cd = MPCOutputFBWithDisturbance(0.2, 20, [0, 0, 0, 3], [0, 0], start, env=env, terminal_set_dir=TERMINAL_SETS,

@@ -76,6 +76,36 @@ def test_outputfb_closed_loop_against_oracle(gpu_available):
     assert abs(sim.state[0] - 30) < 0.5 and abs(sim.state[1] - 1.5) < 0.1
 
 
+def test_step_side_effect_costs(gpu_available):
+    """terminal_cost (absolute x_N, mpc.py:344-345), stage_cost (mpc.py:347) of MPCStateFB.step and cost of
+    MPCOutputFB.step (mpc.py:478, 487) on the GPU path, against the reference formulas at the golden optimum."""
+    from costs import OBJ_RTOL, objective, stage_cost, terminal_cost
+    from oracle import assembly as oa
+    from oracle import qp as oq
+    from carmpc_amd.environments import RoadMultipleCarsEnv
+    from carmpc_amd.mpc import MPCOutputFB, MPCStateFB
+    env = RoadMultipleCarsEnv()
+    asm = oa.build("RoadMultipleCarsEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    g = np.load(os.path.join(GOLDEN, "qp_RoadMultipleCarsEnv_N20.npz"))
+    c = MPCStateFB(0.2, 20, [0, 0, 0, 3], [0, 0], env=env, terminal_set_dir=TERMINAL_SETS)
+    for i in np.where(g["status"] == 0)[0][:6]:
+        x0, us = g["x0"][i], g["u_star"][i]
+        c.step(x0)
+        np.testing.assert_allclose(c.x_horizon, (asm.T @ x0 + asm.S @ us).reshape(-1, 4), rtol=0, atol=1e-6)
+        tc, sc = terminal_cost(asm, x0, us), stage_cost(asm, x0, us, oa.STAGE_COST_Q, oa.STAGE_COST_R)
+        assert abs(c.terminal_cost - tc) <= 1e-7 * max(1.0, abs(tc))
+        assert abs(c.stage_cost - sc) <= 1e-7 * max(1.0, abs(sc))
+    start = np.array([12.0, -1.0, 0.0, 2.0])
+    co = MPCOutputFB(0.2, 20, [0, 0, 0, 3], [0, 0], init_state=start, env=env, terminal_set_dir=TERMINAL_SETS)
+    y = oa.C_OUT @ start + np.array([0.02, -0.01, 0.03])
+    xh = oa.luenberger_observer(asm.A, asm.B, start, np.zeros(2), y)
+    r = oq.solve_instance(asm, xh)
+    assert r["status"] == 0 and r["certified"]
+    co.step(y)
+    j_ref = objective(asm, xh, r["u_exact"])
+    assert abs(co.cost - j_ref) <= OBJ_RTOL * max(1.0, abs(j_ref))
+
+
 def test_step_batch_matches_scalar(gpu_available):
     from carmpc_amd.environments import RoadOneCarEnv
     from carmpc_amd.mpc import MPCStateFB

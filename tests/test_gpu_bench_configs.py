@@ -44,9 +44,12 @@ def _check_sample(asm, X, u, st, idx, xref=None):
     both = (st[idx] == 0) & (sc == 0)
     assert both.sum() > len(idx) // 4
     assert np.abs(u[idx][both] - uc[both]).max() <= U_TOL
+    from costs import OBJ_RTOL, objective_gap
+    assert max(objective_gap(asm, X[i], u[i], uc[k], xref) for k, i in enumerate(idx) if both[k]) <= OBJ_RTOL
     for i in idx[both][:8]:
         r = oq.solve_instance(asm, X[i], xref)
         assert r["certified"] and np.abs(u[i] - r["u_exact"]).max() <= U_TOL
+        assert objective_gap(asm, X[i], u[i], r["u_exact"], xref) <= OBJ_RTOL
 
 
 def test_config5_bench_shard(gpu_available):

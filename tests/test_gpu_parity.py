@@ -2,6 +2,7 @@
 
 Tolerances:
   |u_gpu - u*|_inf <= 1e-6   against the KKT-certified optimum
+  relative objective difference |J(u_gpu) - J(u*)| / max(1, |J(u*)|) <= 1e-9
   constraint violation <= 1e-8, terminal-set rows of x_N <= b + 1e-8
   status identical to the oracle (optimal vs primal-infeasible), except for
   instances whose LP feasibility margin is within 1e-7 of the boundary.
@@ -10,6 +11,7 @@ import numpy as np
 import pytest
 
 from conftest import CONFIGS, GOLDEN, TERMINAL_SETS
+from costs import OBJ_RTOL, objective_gap
 
 pytestmark = pytest.mark.gpu
 
@@ -113,8 +115,9 @@ def test_golden_vectors(gpu_available, name, N, kernel):
     assert ok.any()
     err = np.abs(u[ok] - g["u_star"][ok]).max()
     assert err <= U_TOL, err
-    for x0, uu in zip(g["x0"][ok], u[ok]):
+    for x0, uu, us in zip(g["x0"][ok], u[ok], g["u_star"][ok]):
         assert _violation(asm, x0, uu) <= VIOL_TOL
+        assert objective_gap(asm, x0, uu, us) <= OBJ_RTOL
         xN = (asm.T @ x0 + asm.S @ uu)[-4:]
         tA, tb = asm.term_A[:, -4:], asm.term_b
         assert (tA @ xN - tb).max() <= VIOL_TOL
@@ -157,6 +160,7 @@ def test_random_batch_vs_c_oracle(gpu_available, name, N, kernel):
         r = oq.solve_instance(asm, X[i])
         assert r["certified"]
         assert np.abs(u[i] - r["u_exact"]).max() <= U_TOL
+        assert objective_gap(asm, X[i], u[i], r["u_exact"]) <= OBJ_RTOL
         assert _violation(asm, X[i], u[i]) <= VIOL_TOL
 
 
