@@ -12,7 +12,9 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(HERE, "libcarmpc.so")
-SOURCES = ["capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip", "hetero.hip", "noalloc.hip", "cpu_ipm.hip"]
+SOURCES = ["ipm_riccati_m0.hip", "ipm_riccati_m1.hip", "ipm_riccati_m2.hip", "ipm_riccati_het.hip",    # (slowest first)
+           "capi.hip", "assembly.hip", "ipm_dense.hip", "ipm_staged.hip", "ipm_riccati.hip", "closed_loop.hip", "lp.hip",
+           "hetero.hip", "noalloc.hip", "cpu_ipm.hip"]
 ARCH = os.environ.get("CARMPC_ARCH", "gfx950")
 # -packed-fp32-ops off: hipcc -O3 forms v_pk_*_f32 from ordinary float code by itself and some of
 # their forms have given wrong results on these GPUs; the flag only concerns the device pass (the
@@ -26,7 +28,12 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
 # --amdgpu-mfma-vgpr-form keeps the matrix-core results in ordinary registers: they feed vector
 # FMAs at once, and the default (accumulation-register results) cost ~19 register moves per stage
 # of the factorization pass (10.07M -> 10.35M QP/s).
-FILE_FLAGS = {"ipm_riccati.hip": ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp", "-mllvm", "--amdgpu-mfma-vgpr-form"]}
+# The kernel is instantiated in one translation unit per launch kind (ipm_riccati_m0 / m1 / m2 / het.hip), so
+# that each can have its own flags and the four compile side by side.
+_RIC = ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp", "-mllvm", "--amdgpu-mfma-vgpr-form"]
+# The polish launch's unit keeps the default scheduler: with the iterative-ILP strategy the register allocator of
+# this hipcc (ROCm 7.2.0, clang 22) crashes on its 32-lanes-per-QP instantiation at N = 10.
+FILE_FLAGS = {"ipm_riccati_m0.hip": _RIC, "ipm_riccati_m1.hip": _RIC, "ipm_riccati_m2.hip": _RIC[2:], "ipm_riccati_het.hip": _RIC}
 
 
 def _hipcc():
@@ -43,13 +50,13 @@ def _stale(obj, src, cmd):
     with open(obj + ".cmd") as f:
         if f.read() != " ".join(cmd):
             return True
-    deps = [src, os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h"),
-            os.path.join(REPO, "include", "carmpc.h")]
-    deps += [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".inc")]
+    deps = [src, os.path.join(REPO, "include", "carmpc.h"), os.path.join(CSRC, "carmpc_internal.h"), os.path.join(CSRC, "lanes.h")]
+    if os.path.basename(src).startswith("ipm_riccati"):
+        deps += [os.path.join(CSRC, "ipm_riccati_kernel.h"), os.path.join(CSRC, "ipm_riccati_solve.inc")]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
-def build(verbose: bool = True, jobs: int = 4, variant: str = "") -> str:
+def build(verbose: bool = True, jobs: int = 8, variant: str = "") -> str:
     """Compile csrc/*.hip for gfx950 and link the shared library.  variant="timing"
     builds the phase-timing profiling library build/timing/libcarmpc.so instead."""
     obj_dir = OBJ if not variant else os.path.join(REPO, "build", variant, "obj")

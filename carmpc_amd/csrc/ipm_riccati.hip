@@ -1,1481 +1,22 @@
-// ipm_riccati.hip -- grouped stage-form Mehrotra IPM: 16 lanes per QP, 4 QPs per wavefront.
-//
-// Replaces the per-step cvxpy solve of lib/mpc.py:334-335 / 477-478 with a Mehrotra
-// predictor-corrector IPM (restated on the CPU in oracle/qp.py::ipm), applying M^{-1} by a backward
-// Riccati recursion and a forward roll-out over the horizon (oracle/riccati.py, the CPU restatement
-// this kernel follows line by line).  Every QP row acts on one predicted state x_k (mpc.py:196-253),
-// and H = R_hat + S'Q_hat S (matrix_gen.py:35-72), so
-//     M = H + G'DG + diag(box) = R_hat + diag(Db) + sum_k S_k'(Qbar_k + W_k) S_k.
-//
-// Layout (one QP per 16-lane DPP row; group g = lane>>4, j = lane&15):
-//   * row state in registers: lane j owns stage j+1 (segment 0) and j+17 (segment 1) -- the
-//     rows of those stages sit in its 2 x 8 slots; stage-N rows that do not fit the owner
-//     go to the segments whose stage number exceeds N (capi.hip::riccati_layout);
-//     the owner of stage t+1 also owns the input u_t (both components) and its box rows (LDS);
-//   * stage recursions (adjoints, Riccati factorization, backward/forward solves) exchange
-//     per-stage records in LDS (W_k, rhs, factor K_t / Re_t, y_k, v_t) with the row phases.
-//     Shared-model problems run them on the matrix cores, one 4x4 matrix entry per lane (see
-//     "stage recursions on the matrix cores" below); per-instance models (HET) run them as scalar
-//     code repeated in the 16 lanes of the group;
-//   * per-QP reductions are 16-lane DPP butterflies (lanes.h), bitwise row-uniform.
-// The 4 groups of a wave advance trip by trip together (one trip = one IPM iteration or one
-// polish); a group that finishes an instance claims its next one from an atomic counter at once.
-// Large solves run as three launches of this kernel (MODE, launch pipeline at the end of the file).
-#include "carmpc_internal.h"
-#include "lanes.h"
-
-#include <algorithm>
-#include <cstdlib>
-#include <type_traits>
-
-#include <hip/hip_runtime.h>
-#include <math.h>
-
-// Optional per-phase cycle accounting (profiling build only: -DCARMPC_PHASE_TIMING,
-// tools/ric_timing.py): 0 init, 1 residual rows, 2 adjoint pass, 3 decisions, 4 factor rows,
-// 5 factorization pass, 6 backward passes, 7 forward passes, 8-10 row phases k = 0..2,
-// 11 polish rows.
-#ifdef CARMPC_PHASE_TIMING
-__device__ unsigned long long carmpc_ric_cycles[12];
-#define RT_DECL                                                        \
-    unsigned long long rt_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
-    unsigned long long rt_t = clock64();
-#define RT_MARK(i)                               \
-    do {                                         \
-        const unsigned long long n_ = clock64(); \
-        rt_acc[i] += n_ - rt_t;                  \
-        rt_t = n_;                               \
-    } while (0)
-#define RT_FLUSH()                                                                           \
-    do {                                                                                     \
-        if (lane == 0)                                                                       \
-            for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&carmpc_ric_cycles[i_], rt_acc[i_]); \
-    } while (0)
-#else
-#define RT_DECL
-#define RT_MARK(i) do {} while (0)
-#define RT_FLUSH() do {} while (0)
-#endif
-
-// Unroll factor of the scalar stage loops (per-instance models and the initial roll-out; forward,
-// backward, factorization, adjoint): > 1 lets the compiler rename the one-stage-ahead prefetch
-// registers instead of copying them every stage.  Measured when the shared-model kernels still ran
-// these loops (1 GPU, QP/s) for unroll 1 / 2 / 4 / 5 / 10: 7.05M / 7.52M / 7.73M / 7.80M / 7.76M.
-#ifndef CARMPC_RIC_UNROLL
-#define CARMPC_RIC_UNROLL 5
-#endif
-#ifndef CARMPC_RIC_UNROLL_ADJ
-#define CARMPC_RIC_UNROLL_ADJ 5
-#endif
-// Scalar stage loops: all 16 lanes of a group hold bitwise-identical values (redundant
-// recursions), and every lane stores them (same address, same bits) -- no exec-mask branch
-// per stage.  Lane-0-only stores (CARMPC_RIC_LANE0_WRITE) measured 7.81M vs 8.05M QP/s.
-#ifdef CARMPC_RIC_LANE0_WRITE
-#define RIC_WRITER (j == 0)
-#else
-#define RIC_WRITER true
-#endif
-// Stages of read-ahead of the matrix-core passes (see the comment at kPre).
-#ifndef CARMPC_RIC_KPRE
-#define CARMPC_RIC_KPRE 1
-#endif
-#ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
-                                // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
-#define CARMPC_RIC_UNROLL_HET 1
-#endif
+// ipm_riccati.hip -- launch side of the grouped stage-form IPM kernel (ipm_riccati_kernel.h): grid sizing,
+// dispatch by horizon and model structure, the three-launch pipeline, several problems per launch.
+#include "ipm_riccati_kernel.h"
 
 namespace carmpc {
 
-namespace {
-
-using namespace lanes;
-
-constexpr int G16 = kRicLanes;
-constexpr int RSEG = kRicSeg;
-constexpr int RS = kRicSlots;
-constexpr int REC = 20;   // doubles per stage record (160 B)
-// record t (stage t+1, input t):
-//   [0..9]   W_{t+1} (packed) | lamZ_{t+1} [0..3], lamH_{t+1} [4..7] | factor: K_t [0..7], il00 l10 il11 [8..10]
-//   [12..15] b^x_{t+1} | y_{t+1} | gz_t [12..13], hs_t [14..15]
-//   [16..17] b^u_t | v_t
-//   [18..19] Db_t | kappa_t
-constexpr int O_K = 0, O_CH = 8, O_ZERO = 11, O_BX = 12, O_BU = 16, O_DB = 18;
-
-// The polish is attempted once mu <= POLISH_MU with both residuals within POLISH_RES (relative, like the
-// termination tolerance): far earlier than the IPM would terminate.  An accepted polish is the exact
-// optimum whenever it comes, so the gate only trades iterations saved (about 3 per instance against the
-// conservative gate mu <= 1e-6, residuals within the termination tolerance) for more rejected attempts,
-// most of which the correction round repairs (measured with the conservative first active set below: gates
-// from 5e-5 / 3e-6 to 2e-2 / 3e-4, best from 5e-3 / 1e-4 on; beyond 2e-2 the retry launch outgrows the
-// gain).  Overridable for such sweeps (tools/gpu/mkvar.sh).
-// The per-instance kernels keep the conservative gate, like the fallback kernels.
-#ifndef CARMPC_POLISH_MU
-#define CARMPC_POLISH_MU 1e-2
-#endif
-#ifndef CARMPC_POLISH_RES
-#define CARMPC_POLISH_RES 2e-4
-#endif
-constexpr double POLISH_MU = CARMPC_POLISH_MU, POLISH_RES = CARMPC_POLISH_RES;
-constexpr double POLISH_MU_CONSERVATIVE = 1e-6;
-// First active set of a polish: the rows with s < POLISH_ACT z.  A conservative guess (few rows active, the
-// correction round adds the violated ones) is accepted far more often than s < z: 76 % instead of 50 % at
-// this gate, and 1.7 % instead of 13 % rejected after the correction (swept 0.001..30 for several gates).
-#ifndef CARMPC_POLISH_ACT
-#define CARMPC_POLISH_ACT 0.003
-#endif
-constexpr double POLISH_ACT = CARMPC_POLISH_ACT;
-// Initial point: slacks s = max(w - G u0, INIT_SFLOOR), multipliers on the central path z = mu0 / s with
-// mu0 = clamp((|q|_inf / (INIT_Q_PER_VAR n))^2, INIT_MU_MIN, INIT_MU0): a centred start whose distance from the
-// boundary follows the size of the linear term.  States far from the goal (large q, many active rows at the
-// optimum) start well inside the cone -- about 1.3 iterations fewer than z = 1 with the floor at 1 on the
-// bench's states --, states on closed-loop trajectories and near the goal (little or nothing active) start
-// close to the boundary and keep their 3 to 4 iterations, where a fixed mu0 = 100 costs them 5 (measured:
-// linear and quadratic rules; the best scale is 100..200 at N = 20, 50..70 at N = 10, about 35 at N = 5, hence
-// proportional to the number of variables).  INIT_MU0 = 0 means z = 1 (the per-instance kernels, like the
-// fallback kernels).
-#ifndef CARMPC_INIT_MU0
-#define CARMPC_INIT_MU0 100.0
-#endif
-#ifndef CARMPC_INIT_MU_MIN
-#define CARMPC_INIT_MU_MIN 1.0
-#endif
-#ifndef CARMPC_INIT_Q_PER_VAR
-#define CARMPC_INIT_Q_PER_VAR 3.5
-#endif
-#ifndef CARMPC_INIT_SFLOOR
-#define CARMPC_INIT_SFLOOR 2.0
-#endif
-constexpr double POLISH_DELTA = 1e-10;
-constexpr int POLISH_REFINE = 2;            // refinement passes of the polish solve (2: |u - u*| ~ 1e-10, same acceptances as 3)
-constexpr int POLISH_REFINE_CONSERVATIVE = 3;   // ... of the per-instance kernels, like the fallback kernels
-constexpr double POLISH_TOL = 1e-11;
-
-template <int N>
-struct RicShared {
-    double2 cf01[RS * G16];   // slot (s, j): c~0, c~1
-    double2 cf23[RS * G16];   // c~2, c~3
-    int32_t partner[RS * G16];
-    double lb[64], ub[64];
-};
-// per-input state of the owned inputs, one row of 12 fields x 2 components per input pair t
-// (row N: dummy row written by lanes whose segment owns no input)
-enum { F_U = 0, F_Q, F_SU, F_SL, F_ZU, F_ZL, F_RD, F_E1, F_E2, F_E3, F_E4, F_VX, F_COUNT };
-template <int N>
-struct RicWave {
-    // stage records of the 4 groups; the polish verification scratch [RS][64] aliases them
-    double recbuf[4 * N * REC > RS * 64 ? 4 * N * REC : RS * 64];
-    double w[RS][64];         // w = w0 - E x0 per (slot, lane)
-    double vbox[4][N + 1][F_COUNT * 2];
-};
-
-__device__ __forceinline__ void wb() { __builtin_amdgcn_wave_barrier(); }
-
-// Compile-time sparsity of the stage matrices: entries outside a mask are exactly zero and,
-// with AUNIT, diag(A) == 1 exactly (verified on the host, capi.hip::riccati_layout), so the
-// unrolled products skip them.  DenseModel is the general fallback.
-constexpr unsigned bit4(int a, int b) { return 1u << (a * 4 + b); }
-constexpr unsigned bit2(int a, int b) { return 1u << (a * 2 + b); }
-struct DenseModel {
-    static constexpr unsigned A = 0xFFFFu, B = 0xFFu, Q = 0xFFFFu, R = 0xFu;
-    static constexpr bool AUNIT = false;
-};
-// kinematic bicycle linearised and discretised as in mpc.py:128-180: A = I + dt A_lin with
-// A_lin nonzero only in rows 0-1 (columns 2-3) and entry (2,3); B = dt B_lin with B_lin[2][1],
-// B_lin[3][0]; Q, R diagonal (configuration.py:19-21).
-struct BicycleModel {
-    static constexpr unsigned A = bit4(0, 0) | bit4(0, 2) | bit4(0, 3) | bit4(1, 1) | bit4(1, 2) | bit4(1, 3) |
-                                  bit4(2, 2) | bit4(2, 3) | bit4(3, 3);
-    static constexpr unsigned B = bit2(2, 1) | bit2(3, 0);
-    static constexpr unsigned Q = bit4(0, 0) | bit4(1, 1) | bit4(2, 2) | bit4(3, 3);
-    static constexpr unsigned R = bit2(0, 0) | bit2(1, 1);
-    static constexpr bool AUNIT = true;
-};
-template <class SP>
-struct Mt {
-    const StageMats& m;
-    // acc + X[a][b] * x, skipping structural zeros (indices are unrolled constants)
-    __device__ __forceinline__ double A_(int a, int b, double x, double acc) const {
-        if (!((SP::A >> (a * 4 + b)) & 1u)) return acc;
-        if (SP::AUNIT && a == b) return acc + x;
-        return fma(m.A[a * 4 + b], x, acc);
-    }
-    __device__ __forceinline__ double B_(int a, int c, double x, double acc) const {
-        return ((SP::B >> (a * 2 + c)) & 1u) ? fma(m.B[a * 2 + c], x, acc) : acc;
-    }
-    __device__ __forceinline__ double Q_(int a, int b, double x, double acc) const {
-        return ((SP::Q >> (a * 4 + b)) & 1u) ? fma(m.Q[a * 4 + b], x, acc) : acc;
-    }
-    __device__ __forceinline__ double R_(int c, int d, double x, double acc) const {
-        return ((SP::R >> (c * 2 + d)) & 1u) ? fma(m.R[c * 2 + d], x, acc) : acc;
-    }
-    // structural zeros are returned / accumulated as -0.0: x + (-0.0) == x and
-    // fma(a, b, -0.0) == a * b exactly, so the compiler drops them
-    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : -0.0; }
-    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : -0.0; }
-    // (R v)_c
-    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, -0.0)); }
-};
-
-// Per-instance model (carmpc_hetero_*): A, B of the group's own instance in registers (only the
-// entries inside the sparsity masks are ever read), Q, R shared from the kernel argument.
-template <class SP>
-struct MtH {
-    const StageMats& m;
-    double A[16], B[8];
-    __device__ explicit MtH(const StageMats& s) : m(s), A{}, B{} {}
-    __device__ __forceinline__ double A_(int a, int b, double x, double acc) const {
-        if (!((SP::A >> (a * 4 + b)) & 1u)) return acc;
-        if (SP::AUNIT && a == b) return acc + x;
-        return fma(A[a * 4 + b], x, acc);
-    }
-    __device__ __forceinline__ double B_(int a, int c, double x, double acc) const {
-        return ((SP::B >> (a * 2 + c)) & 1u) ? fma(B[a * 2 + c], x, acc) : acc;
-    }
-    __device__ __forceinline__ double Q_(int a, int b, double x, double acc) const {
-        return ((SP::Q >> (a * 4 + b)) & 1u) ? fma(m.Q[a * 4 + b], x, acc) : acc;
-    }
-    __device__ __forceinline__ double R_(int c, int d, double x, double acc) const {
-        return ((SP::R >> (c * 2 + d)) & 1u) ? fma(m.R[c * 2 + d], x, acc) : acc;
-    }
-    __device__ __forceinline__ double Qv(int a, int b) const { return ((SP::Q >> (a * 4 + b)) & 1u) ? m.Q[a * 4 + b] : -0.0; }
-    __device__ __forceinline__ double Rv(int c, int d) const { return ((SP::R >> (c * 2 + d)) & 1u) ? m.R[c * 2 + d] : -0.0; }
-    __device__ __forceinline__ double Rmul(int c, double v0, double v1) const { return R_(c, 0, v0, R_(c, 1, v1, -0.0)); }
-};
-
-// HET: every instance has its own linearisation (hetero.hip): A, B, P, slot row norms, w0, E,
-// hq and x0-only rows come from the instance's slices; the row layout is the template's.
-// One launch serves up to kRicMaxSeg problems (instance segments, carmpc_solve_segments); a
-// single problem is the one-segment case.  The descriptors travel by value in the kernel arguments
-// (scalar loads), every segment has its own claim counter (S.claim + 16 seg), and the workgroups
-// are dealt to "home" segments in proportion to the instance counts.  A workgroup serves its home
-// segment until that counter runs out, then moves on round-robin to help with the others
-// (reloading the problem's slot tables), so the launch ends when every segment is drained -- no
-// per-problem launch tail, no side streams.
-//
-// MODE splits the solve over three launches (launch pipeline below) so that each one runs lean code:
-//   1  interior-point iterations only.  An instance that reaches its polish point is handed off --
-//      its active set (one bit per row slot and box row) and iteration count go to the work lists --
-//      and the group claims its next instance at once.  No polish code, no polish state.
-//   2  polish only, over the hand-off list: every instance runs the same fixed sequence (active-set
-//      factorization, solve, three refinements, acceptance test), so the four groups of a wave polish
-//      in lock-step instead of one at a time beside three iterating groups.  A group whose polish
-//      is rejected keeps the instance for the correction round (its next trip, see act_next); what
-//      is rejected again goes to the retry list.
-//   0  the complete algorithm in one kernel (iterations and polish interleaved per group): solves the
-//      retry list from scratch -- the arithmetic is deterministic, so this reproduces the rejected
-//      polish and carries on exactly as a single-kernel solve would -- and serves callers that bring
-//      their own instance lists or claim counter (closed loops, per-instance models, no-allocation entry).
-template <int N, int WPB, class SP, bool HET = false, int MODE = 0>
-__global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWork W, const double* __restrict__ x0_all,
-                                                               const double* __restrict__ xref_all,
-                                                               double* __restrict__ u_all, int64_t ld_u,
-                                                               int32_t* __restrict__ status_all,
-                                                               int32_t* __restrict__ iters_all, Settings S_all) {
-    static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
-    constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
-    constexpr int kPolRefine = HET ? POLISH_REFINE_CONSERVATIVE : POLISH_REFINE;
-    constexpr double kAct = HET ? 1.0 : POLISH_ACT;   // a row starts the polish active when s < kAct z
-    constexpr int kSolves = kPolRefine + 1 > 3 ? kPolRefine + 1 : 3;   // solves per trip: 3 of a step, kPolRefine + 1 of a polish
-    constexpr double kMuMin = CARMPC_INIT_MU_MIN, kQInv = 1.0 / (CARMPC_INIT_Q_PER_VAR * 2 * N);
-    constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
-    constexpr int kUnrollAdj = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL_ADJ;
-    __shared__ __attribute__((aligned(16))) RicShared<N> sh;
-    __shared__ __attribute__((aligned(16))) RicWave<N> wscr[WPB];
-    const int nseg = T.nseg;
-    int home = 0;
-    if (nseg > 1) {
-        const int64_t first = T.off[0], total = T.off[nseg] - first;
-        const int64_t pos = first + (int64_t)blockIdx.x * total / gridDim.x;
-        while (home + 1 < nseg && pos >= T.off[home + 1]) ++home;
-    }
-    for (int kseg_i = 0; kseg_i < nseg; ++kseg_i) {
-    const int seg = nseg > 1 ? (home + kseg_i) % nseg : 0;
-    const DevProblem& P = T.P[seg];
-    const int64_t seg0 = T.off[seg], batch = T.off[seg + 1] - seg0;
-    const int64_t lst0 = seg0 - T.off[0];   // the segment's start in the work lists, which begin at the run's first instance
-    const double* __restrict__ x0 = x0_all + seg0 * NX;
-    const double* __restrict__ xref = xref_all ? xref_all + seg0 * NX : nullptr;
-    double* __restrict__ u_out = u_all + seg0 * ld_u;
-    int32_t* __restrict__ status_out = status_all + seg0;
-    int32_t* __restrict__ iters_out = iters_all ? iters_all + seg0 : nullptr;
-    Settings S = S_all;
-    if (W.cnt) {   // launch pipeline: this segment's counters and work lists of round W.round (RicWork)
-        unsigned* wc = W.cnt + kRicClaimStride * seg;
-        if constexpr (MODE == 1) {
-            if (W.round == 0) {
-                S.claim = wc + 0;
-            } else {   // the previous round's rejected polishes
-                S.index = W.retry_idx + lst0;
-                S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
-                S.claim = wc + 4 * W.round;
-            }
-        } else if constexpr (MODE == 2) {
-            S.index = nullptr;   // (rows come from the hand-off records)
-            S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round + 1);
-            S.claim = wc + 4 * W.round + 2;
-        } else {   // after the last round
-            S.index = W.retry_idx + lst0;
-            S.count = reinterpret_cast<const int32_t*>(wc + 4 * W.round - 1);
-            S.claim = wc + 4 * W.round;
-        }
-    } else if (S.claim) {
-        S.claim += kRicClaimStride * seg;
-    }
-    if (kseg_i > 0) __syncthreads();   // every wave is done with the previous problem's tables
-    if (batch <= 0) continue;
-    const StageMats& MT = P.mats;
-    std::conditional_t<HET, MtH<SP>, const Mt<SP>> M{P.mats};
-    int64_t hinst = 0;   // HET: the group's current instance (slice index)
-    for (int i = threadIdx.x; i < RS * G16; i += blockDim.x) {
-        sh.cf01[i] = make_double2(P.r_coef[i * 4 + 0], P.r_coef[i * 4 + 1]);
-        sh.cf23[i] = make_double2(P.r_coef[i * 4 + 2], P.r_coef[i * 4 + 3]);
-        sh.partner[i] = P.r_partner ? P.r_partner[i] : -1;
-    }
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) {
-        const bool bx = i < 2 * N && P.boxed;
-        sh.lb[i] = bx ? P.lb[i] : -UNBOXED_BOUND;
-        sh.ub[i] = bx ? P.ub[i] : UNBOXED_BOUND;
-    }
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int g = lane >> 4, j = lane & 15;
-    RicWave<N>& wv = wscr[wave];
-    double* rec = wv.recbuf + g * (N * REC);
-    double(*scr)[64] = reinterpret_cast<double(*)[64]>(wv.recbuf);
-    const bool boxed = P.boxed != 0;
-    // segment stages: seg 0 -> j+1, seg 1 -> j+17 (overflow segments -> stage N)
-    int kseg[2];
-    bool own[2], isN[2];
-#pragma unroll
-    for (int sg = 0; sg < 2; ++sg) {
-        const int k = j + 1 + 16 * sg;
-        own[sg] = k <= N;
-        kseg[sg] = k <= N ? k : N;
-        isN[sg] = kseg[sg] == N;
-    }
-    double* vb[2];
-#pragma unroll
-    for (int sg = 0; sg < 2; ++sg) vb[sg] = &wv.vbox[g][own[sg] ? kseg[sg] - 1 : N][0];
-#define BX(F, sg, c) vb[sg][(F) * 2 + (c)]
-    // Unused row slots are made inert instead of being masked: their coefficients are zero, w = 1,
-    // s = 1, z = 0, so every residual, direction and sum below gets an exact zero from them and the
-    // slot loops are straight-line code (no exec-mask region per slot).  The validity bits are only
-    // consulted where the instance is set up and in the polish acceptance test.
-    unsigned rvm = 0;
-#pragma unroll
-    for (int s = 0; s < RS; ++s) rvm |= (P.r_valid[s * G16 + j] != 0 ? 1u : 0u) << s;
-    auto valid = [&](int s) { return ((rvm >> s) & 1u) != 0; };
-    const int p = P.p;
-    const int m_rows = p + (boxed ? 4 * N : 0);
-    const double inv_m = 1.0 / (double)(m_rows > 0 ? m_rows : 1);
-    const double idl = 1.0 / POLISH_DELTA;
-
-    // ---- helpers ----------------------------------------------------------------------
-    // Row-slot loops.  Slots are visited pairwise -- slot i of segment 0, then slot i of segment 1 --
-    // for i below the problem's slots-per-segment count (wave-uniform: a scalar branch ahead of the
-    // pairs i >= kSegMin, none below).  The next slot's coefficients and w are loaded one slot ahead
-    // and a scheduling barrier closes every slot: the live set stays one slot wide instead of
-    // growing with however many slots the compiler chooses to interleave.
-    struct SlotIn { double2 c01, c23; double w, iv; };
-    auto ld_slot = [&](int s) __attribute__((always_inline)) {
-        SlotIn in;
-        in.c01 = sh.cf01[s * G16 + j];
-        in.c23 = sh.cf23[s * G16 + j];
-        in.w = wv.w[s][lane];
-        in.iv = 1.0;
-        if constexpr (HET) in.iv = P.het_ric_invn[hinst * (RS * G16) + s * G16 + j];
-        return in;
-    };
-    auto coef = [&](const SlotIn& in, double (&c)[4]) __attribute__((always_inline)) {
-        c[0] = in.c01.x; c[1] = in.c01.y; c[2] = in.c23.x; c[3] = in.c23.y;
-        if constexpr (HET) {   // raw template coefficients x this instance's 1/||G_r||
-#pragma unroll
-            for (int a2 = 0; a2 < 4; ++a2) c[a2] *= in.iv;
-        }
-    };
-    constexpr int kSegMin = 6;
-    const int rseg = P.rseg;
-    auto for_slots = [&](auto&& body) __attribute__((always_inline)) {
-        SlotIn cur = ld_slot(0);
-#pragma unroll
-        for (int q = 0; q < RS; ++q) {
-            const int i = q >> 1, s = (q & 1) * RSEG + i;
-            if (i >= kSegMin && i >= rseg) break;   // uniform; the remaining slots are unused in every lane
-            const int qn = q + 1 < RS ? q + 1 : q;
-            const SlotIn nxt = ld_slot((qn & 1) * RSEG + (qn >> 1));
-            body(s, cur);
-            __builtin_amdgcn_sched_barrier(0);
-            cur = nxt;
-        }
-    };
-    // the same visit without the loads (slot state in registers only)
-    auto for_used = [&](auto&& body) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < RS; ++q) {
-            const int i = q >> 1;
-            if (i >= kSegMin && i >= rseg) break;
-            body((q & 1) * RSEG + i);
-        }
-    };
-#define FOR_SLOTS_BEGIN                                                                        \
-    for_slots([&](const int s, const SlotIn& in) __attribute__((always_inline)) {              \
-        const int sg = s / RSEG;                                                               \
-        double c[4];                                                                           \
-        coef(in, c);
-#define FOR_SLOTS_END });
-    auto cf = [&](int s, double (&c)[4]) {
-        const double2 a = sh.cf01[s * G16 + j], b = sh.cf23[s * G16 + j];
-        c[0] = a.x; c[1] = a.y; c[2] = b.x; c[3] = b.y;
-        if constexpr (HET) {   // raw template coefficients x this instance's 1/||G_r||
-            const double iv = P.het_ric_invn[hinst * (RS * G16) + s * G16 + j];
-#pragma unroll
-            for (int a2 = 0; a2 < 4; ++a2) c[a2] *= iv;
-        }
-    };
-    // terminal cost P (upper triangle read): shared, or this instance's DARE solution
-    auto Pv = [&](int idx) -> double {
-        if constexpr (HET) return P.het_P[hinst * 16 + idx];
-        else return MT.P[idx];
-    };
-    auto dot4 = [&](const double (&c)[4], const double (&y)[4]) {
-        return fma(c[3], y[3], fma(c[2], y[2], fma(c[1], y[1], c[0] * y[0])));
-    };
-    auto rd4 = [&](int off, double (&v)[4]) {   // rec[off..off+3]
-        const double2 a = *reinterpret_cast<const double2*>(rec + off);
-        const double2 b = *reinterpret_cast<const double2*>(rec + off + 2);
-        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
-    };
-    auto wr4 = [&](int off, const double (&v)[4]) {
-        *reinterpret_cast<double2*>(rec + off) = make_double2(v[0], v[1]);
-        *reinterpret_cast<double2*>(rec + off + 2) = make_double2(v[2], v[3]);
-    };
-    auto rd2 = [&](int off, double& a, double& b) {
-        const double2 v = *reinterpret_cast<const double2*>(rec + off);
-        a = v.x; b = v.y;
-    };
-    auto rdK = [&](int r, double (&K)[8]) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const double2 v = *reinterpret_cast<const double2*>(rec + r + O_K + 2 * e);
-            K[2 * e] = v.x;
-            K[2 * e + 1] = v.y;
-        }
-    };
-    auto wr2 = [&](int off, double a, double b) { *reinterpret_cast<double2*>(rec + off) = make_double2(a, b); };
-    // y += Qbar_k v (k runtime, 1..N) -- only segment owners call it
-    auto add_qbar = [&](bool termN, const double (&v)[4], double (&y)[4], double sgn) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            double accp = -0.0, accq = -0.0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                accp = fma(Pv((a < b ? a : b) * 4 + (a < b ? b : a)), v[b], accp);
-                accq = M.Q_(a, b, v[b], accq);
-            }
-            y[a] = fma(sgn, termN ? accp : accq, y[a]);
-        }
-    };
-    // sum the stage-N partials of the 16 lanes; owners write b^x (plus Qbar term) of their stages
-    auto write_bx = [&](double (&acc)[2][4], const double (&qv)[2][4], double qsgn) {
-        double pn[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) pn[a] = (isN[0] ? acc[0][a] : 0.0) + (isN[1] ? acc[1][a] : 0.0);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) pn[a] = row_sum(pn[a]);
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) {
-            if (own[sg]) {
-                double v[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) v[a] = isN[sg] ? pn[a] : acc[sg][a];
-                if (qsgn != 0.0) add_qbar(kseg[sg] == N, qv[sg], v, qsgn);
-                wr4((kseg[sg] - 1) * REC + O_BX, v);
-            }
-        }
-    };
-
-    // ---- stage recursions (redundant in the 16 lanes of a group) ----------------------
-    // backward linear pass: p_N = b^x_N; g_t = b^u_t + B'p_{t+1}; kappa_t = Re_t^{-1} g_t;
-    // p_t = b^x_t + A'p_{t+1} - K_t'g_t   (oracle/riccati.py::riccati_solve)
-    auto back_linear = [&]() {
-        wb();
-        double pv[4];
-        rd4((N - 1) * REC + O_BX, pv);
-        // stage data one stage ahead (software pipelining of the LDS latency)
-        auto ld = [&](int t, double (&bu)[2], double (&ch)[4], double (&K)[8], double (&bx)[4]) {
-            const int r = t * REC;
-            rd2(r + O_BU, bu[0], bu[1]);
-            rd2(r + O_CH, ch[0], ch[1]);
-            rd2(r + O_CH + 2, ch[2], ch[3]);
-            rdK(r, K);
-            rd4((t >= 1 ? r - REC : 0) + O_BX, bx);
-        };
-        double bu[2], ch[4], K[8], bx[4];
-        ld(N - 1, bu, ch, K, bx);
-#pragma unroll kUnroll
-        for (int t = N - 1; t >= 0; --t) {
-            double nbu[2], nch[4], nK[8], nbx[4];
-            ld(t >= 1 ? t - 1 : 0, nbu, nch, nK, nbx);
-            double g0 = bu[0], g1 = bu[1];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                g0 = M.B_(a, 0, pv[a], g0);
-                g1 = M.B_(a, 1, pv[a], g1);
-            }
-            const double il00 = ch[0], l10 = ch[1], il11 = ch[2];
-            const double y0 = g0 * il00;
-            const double y1 = fma(-l10, y0, g1) * il11;
-            const double k1 = y1 * il11;
-            const double k0 = fma(-l10, k1, y0) * il00;
-            if (RIC_WRITER) wr2(t * REC + O_DB, k0, k1);
-            double np[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                double acc = bx[a];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
-                acc = fma(-K[a], g0, acc);
-                np[a] = fma(-K[4 + a], g1, acc);
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) pv[a] = np[a];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) K[e] = nK[e];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { ch[e] = nch[e]; bx[e] = nbx[e]; }
-            bu[0] = nbu[0];
-            bu[1] = nbu[1];
-        }
-        wb();
-    };
-    // forward pass: y_0 = 0; v_t = kappa_t - K_t y_t; y_{t+1} = A y_t + B v_t -> rec
-    auto forward = [&]() {
-        wb();
-        double y[4] = {0.0, 0.0, 0.0, 0.0};
-        double K[8], kp[2];
-        rdK(0, K);
-        rd2(O_DB, kp[0], kp[1]);
-#pragma unroll kUnroll
-        for (int t = 0; t < N; ++t) {
-            const int r = t * REC;
-            const int rn = (t + 1 < N ? t + 1 : t) * REC;
-            double nK[8], nkp[2];
-            rdK(rn, nK);
-            rd2(rn + O_DB, nkp[0], nkp[1]);
-            double v0 = kp[0], v1 = kp[1];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                v0 = fma(-K[a], y[a], v0);
-                v1 = fma(-K[4 + a], y[a], v1);
-            }
-            double ny[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                double acc = M.B_(a, 0, v0, -0.0);
-                acc = M.B_(a, 1, v1, acc);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
-                ny[a] = acc;
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) y[a] = ny[a];
-            if (RIC_WRITER) {
-                wr4(r + O_BX, y);
-                wr2(r + O_BU, v0, v1);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) K[e] = nK[e];
-            kp[0] = nkp[0];
-            kp[1] = nkp[1];
-        }
-        wb();
-    };
-    // plain roll-out of v_t stored in rec[t][O_BU] (initial point): y -> rec[t][O_BX]
-    auto rollout = [&]() {
-        wb();
-        double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll kUnroll
-        for (int t = 0; t < N; ++t) {
-            const int r = t * REC;
-            double v0, v1;
-            rd2(r + O_BU, v0, v1);
-            double ny[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                double acc = M.B_(a, 0, v0, -0.0);
-                acc = M.B_(a, 1, v1, acc);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
-                ny[a] = acc;
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) y[a] = ny[a];
-            wb();
-            if (RIC_WRITER) wr4(r + O_BX, y);
-        }
-        wb();
-    };
-    // Riccati factorization with W_k, Db_t from rec, fused with the backward linear pass
-    // of the first right-hand side (b^x, b^u in rec)   (oracle/riccati.py::riccati_factor)
-    auto factor_and_back = [&]() {
-        wb();
-        double Pm[10], pv[4];
-        {
-            double Wn[10];
-#pragma unroll
-            for (int e = 0; e < 5; ++e) rd2((N - 1) * REC + 2 * e, Wn[2 * e], Wn[2 * e + 1]);
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = a; b < 4; ++b) Pm[sym10(a, b)] = Pv(a * 4 + b) + Wn[sym10(a, b)];
-            rd4((N - 1) * REC + O_BX, pv);
-        }
-        // stage data one stage ahead: Db_t, b^u_t (record t), W_t, b^x_t (record t-1)
-        auto ld = [&](int t, double (&du)[4], double (&Wt)[10], double (&bx)[4]) {
-            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
-            rd2(r + O_DB, du[0], du[1]);
-            rd2(r + O_BU, du[2], du[3]);
-#pragma unroll
-            for (int e = 0; e < 5; ++e) rd2(rp + 2 * e, Wt[2 * e], Wt[2 * e + 1]);
-            rd4(rp + O_BX, bx);
-        };
-        double du[4], Wt[10], bx[4];
-        ld(N - 1, du, Wt, bx);
-#pragma unroll kUnroll
-        for (int t = N - 1; t >= 0; --t) {
-            const int r = t * REC;
-            double ndu[4], nWt[10], nbx[4];
-            ld(t >= 1 ? t - 1 : 0, ndu, nWt, nbx);
-            const double db0 = du[0], db1 = du[1], bu0 = du[2], bu1 = du[3];
-            // PB = P B (4x2); Re = R + diag(Db) + B'PB; F = B'PA = (PB)'A
-            double PB[4][2];
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    double acc = -0.0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) acc = M.B_(b, c, Pm[sym10(a, b)], acc);
-                    PB[a][c] = acc;
-                }
-            double re00 = M.Rv(0, 0) + db0, re10 = M.Rv(1, 0), re11 = M.Rv(1, 1) + db1;
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                re00 = M.B_(a, 0, PB[a][0], re00);
-                re10 = M.B_(a, 1, PB[a][0], re10);
-                re11 = M.B_(a, 1, PB[a][1], re11);
-            }
-            double F[2][4];
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-                for (int mm = 0; mm < 4; ++mm) {
-                    double acc = -0.0;
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) acc = M.A_(a, mm, PB[a][c], acc);
-                    F[c][mm] = acc;
-                }
-            // guarded 2x2 Cholesky (non-positive pivot -> 1e128, as qp._chol_guarded)
-            double p0 = re00;
-            if (!(p0 > 0.0)) p0 = 1e128;
-            const double il00 = frsq(p0);
-            const double l10 = re10 * il00;
-            double p1 = fma(-l10, l10, re11);
-            if (!(p1 > 0.0)) p1 = 1e128;
-            const double il11 = frsq(p1);
-            double K[2][4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const double y0 = F[0][m] * il00;
-                const double y1 = fma(-l10, y0, F[1][m]) * il11;
-                K[1][m] = y1 * il11;
-                K[0][m] = fma(-l10, K[1][m], y0) * il00;
-            }
-            double g0 = bu0, g1 = bu1;
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                g0 = M.B_(a, 0, pv[a], g0);
-                g1 = M.B_(a, 1, pv[a], g1);
-            }
-            const double y0 = g0 * il00;
-            const double y1 = fma(-l10, y0, g1) * il11;
-            const double k1 = y1 * il11;
-            const double k0 = fma(-l10, k1, y0) * il00;
-            wb();
-            if (RIC_WRITER) {
-                wr4(r + O_K, K[0]);
-                wr4(r + O_K + 4, K[1]);
-                wr2(r + O_CH, il00, l10);
-                wr2(r + O_CH + 2, il11, 0.0);
-                wr2(r + O_DB, k0, k1);
-            }
-            if (t >= 1) {
-                // P_t = Qbar_t + W_t + A'PA - F'K  (upper triangle), PA one column at a time
-                double Pn[10];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    double col[4];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        double acc = -0.0;
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) acc = M.A_(d, b, Pm[sym10(c, d)], acc);
-                        col[c] = acc;
-                    }
-#pragma unroll
-                    for (int a = 0; a <= b; ++a) {
-                        double acc = M.Qv(a, b) + Wt[sym10(a, b)];
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) acc = M.A_(c, a, col[c], acc);
-                        acc = fma(-F[0][a], K[0][b], acc);
-                        Pn[sym10(a, b)] = fma(-F[1][a], K[1][b], acc);
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 10; ++e) Pm[e] = Pn[e];
-                double np[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    double acc = bx[a];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc = M.A_(c, a, pv[c], acc);
-                    acc = fma(-K[0][a], g0, acc);
-                    np[a] = fma(-K[1][a], g1, acc);
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a) pv[a] = np[a];
-            }
-#pragma unroll
-            for (int e = 0; e < 10; ++e) Wt[e] = nWt[e];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { du[e] = ndu[e]; bx[e] = nbx[e]; }
-        }
-        wb();
-    };
-
-
-    // ---- stage recursions on the matrix cores (shared-model problems) -------------------
-    // v_mfma_f64_4x4x4f64 multiplies four independent 4x4 blocks per wavefront; block b lives in
-    // lanes 16 r + 4 b + c (r, c = 0..3), and with X^ the 4x4 matrix whose entry (r, c) is the
-    // value lane (r, c) holds in register X, the instruction computes  D^ = A^' B^ + C^
-    // (operand A enters transposed; the neg modifier negates an operand for free).  In the
-    // recursion phases block b therefore works on QP group b with ONE matrix entry per lane --
-    // P, K, the 2x2 pivots are single registers -- instead of every lane of a group repeating the
-    // whole 4x4 recursion; vectors are 4x4 operands whose columns all hold the vector (the adjoint
-    // pass carries psiZ / psiH in columns 0 / 1).  Stage data is exchanged with the row phases
-    // through the same LDS records.  The passes are straight-line code without exec masking:
-    //   * all four blocks always compute (MFMA needs the whole wave); a block whose group sits out
-    //     a pass only overwrites record fields that are dead until the group's next trip;
-    //   * structural zeros (rows 2-3 of K, of b^u, ...) are loaded from slot 11 of each record,
-    //     which always holds 0.0, and lanes whose result is a structural zero store it there;
-    //   * lanes that hold copies of one value (the columns of a vector) all store it.
-    const int mb = (lane >> 2) & 3, mr = lane >> 4, mc = lane & 3;
-    double* recm = wv.recbuf + mb * (N * REC);
-    auto mm = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0); };
-    auto mm_na = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1); };
-    const bool m_top = mr < 2, m_left = mc < 2;
-    const int oW = sym10(mr, mc);                              // W^, P^ entry in the packed 10-vector
-    const int oK = m_top ? O_K + 4 * mr + mc : O_ZERO;         // K^ (rows 0-1)
-    const int oKT = m_left ? O_K + 4 * mc + mr : O_ZERO;       // K'^ (columns 0-1)
-    const int oLam = m_left ? 4 * mc + mr : O_ZERO;            // [lamZ lamH 0 0]
-    const int oGH = (m_top && m_left) ? 12 + 2 * mc + mr : O_ZERO;   // gz, hs
-    const int oBUt = m_top ? O_BU + mr : O_ZERO;               // b^u / v in rows 0-1
-    const int oBU1 = mr == 1 ? O_BU : O_ZERO;                  // b^u_0 in row 1 (for E b^u)
-    const int oKPt = m_top ? O_DB + mr : O_ZERO;               // kappa in rows 0-1
-    const int oDrow = O_CH + (mr == 0 ? 1 : 2);                // 1/p0 in row 0, 1/p1 below
-    double cA = 0.0, cBp = 0.0, cB0r = 0.0, cB1r = 0.0, cQ = 0.0, cPt = 0.0;
-    if constexpr (!HET) {
-        cA = MT.A[mr * 4 + mc];                       // A^
-        cBp = m_left ? MT.B[mr * 2 + mc] : 0.0;       // [B 0 0]^
-        cB0r = MT.B[mr * 2];                          // column 0 of B in every column
-        cB1r = MT.B[mr * 2 + 1];                      // column 1 of B in every column
-        cQ = MT.Q[mr * 4 + mc];
-        cPt = MT.P[mr * 4 + mc];
-    }
-    // Constants that only one kind of pass needs are rebuilt at its start (a dozen instructions, or two
-    // matrix-core transposes) instead of occupying registers through the row phases; the lane index goes
-    // through an empty asm so that the compiler does not hoist them back out of the trip loop.
-    struct PassK { double cB0m1, k10, kd, cI; };
-    auto pass_consts = [&]() __attribute__((always_inline)) {
-        int lz = lane;
-        asm volatile("" : "+v"(lz));
-        const int r_ = lz >> 4, c_ = lz & 3;
-        PassK k;
-        k.cB0m1 = c_ == 1 ? cB0r : 0.0;                          // column 0 of B in column 1
-        k.k10 = (r_ == 1 && c_ == 0) ? 1.0 : 0.0;
-        k.kd = (r_ == c_ && r_ < 2) ? 1.0 : 0.0;                 // identity of the leading 2x2 block
-        k.cI = r_ == c_ ? 1.0 : 0.0;
-        return k;
-    };
-    // One wave per SIMD leaves nothing to hide an LDS round trip (~70 cycles) or an MFMA result
-    // (28 cycles to a dependent MFMA, 16 cycles of pipe each) behind, so the passes are software
-    // pipelined by hand: stage t's record fields are read kPre stages ahead, side products and
-    // stores trail the recursion by a stage, and a scheduling barrier closes every stage -- without
-    // it the compiler sinks the stores (nothing waits for them) and, since it cannot rule out an
-    // alias between lane-dependent LDS offsets, every later load sinks behind them, back onto the
-    // critical path.  The loops are fully unrolled; staged values sit in registers.
-    constexpr int kPre = CARMPC_RIC_KPRE;
-    auto stage_fence = [] { __builtin_amdgcn_sched_barrier(0); };
-    // adjoint pass: psi_k = lam_k + A'psi_{k+1} for lamZ (column 0) and lamH (column 1);
-    // gz_t, hs_t = B'psi_{t+1} -> rec[t][12..15]
-    auto adjoint_mm = [&]() __attribute__((always_inline)) {
-        wb();
-        double lam[N], psi[N + 1], gh[N];
-        psi[N] = 0.0;
-#pragma unroll
-        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) lam[t] = recm[t * REC + oLam];
-        stage_fence();
-#pragma unroll
-        for (int t = N - 1; t >= -2; --t) {
-            if (t - kPre >= 0) lam[t - kPre] = recm[(t - kPre) * REC + oLam];
-            if (t >= 0) psi[t] = mm(cA, psi[t + 1], lam[t]);
-            if (t + 1 >= 0 && t + 1 < N) gh[t + 1] = mm(cBp, psi[t + 1], 0.0);
-            if (t + 2 < N) recm[(t + 2) * REC + oGH] = gh[t + 2];
-            stage_fence();
-        }
-        wb();
-    };
-    // Riccati factorization (W_k, Db_t in rec) fused with the backward pass of the first
-    // right-hand side.  Re_t = R + Db_t + B'PB = L D^{-1} L' with L = [[1, 0], [l, 1]] and
-    // D = diag(1/p0, 1/p1), guarded like the Cholesky it replaces (a non-positive pivot becomes
-    // 1e128), and Re_t^{-1} = E'D E with E = L^{-1} is applied in that factored form -- E F first,
-    // then D, then E' -- never as an explicit inverse: when B'PB is nearly singular the rows of
-    // F = B'PA are nearly dependent, and only the factored form subtracts them before scaling (an
-    // explicit inverse stalled the IPM on such instances).  The three entries of Re_t come out of
-    // MFMAs with B's columns replicated, so every lane of the block holds them (no cross-lane
-    // broadcast).  K_t -> rec[t][0..7], (l, 1/p0, 1/p1) -> rec[t][8..10], kappa_t -> rec[t][18..19]
-    auto factor_mm = [&]() __attribute__((always_inline)) {
-        wb();
-        const PassK pk = pass_consts();
-        const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
-        struct In { double db0, db1, buT, bu01, Wt, bxv; };
-        struct Out { double En, Z, zg, l, drow; };
-        In in[N];
-        Out o[N];
-        auto load = [&](int t) {
-            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
-            in[t].db0 = recm[r + O_DB];
-            in[t].db1 = recm[r + O_DB + 1];
-            in[t].buT = recm[r + oBUt];
-            in[t].bu01 = recm[r + oBU1];
-            in[t].Wt = recm[rp + oW];
-            in[t].bxv = recm[rp + O_BX + mr];
-        };
-        double Pm = cPt + recm[(N - 1) * REC + oW];
-        double pv = recm[(N - 1) * REC + O_BX + mr];
-#pragma unroll
-        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) load(t);
-        stage_fence();
-#pragma unroll
-        for (int t = N - 1; t >= -1; --t) {
-            if (t - kPre >= 0) load(t - kPre);
-            if (t >= 0) {
-                const double T = mm(Pm, cA, 0.0);             // P A
-                const double PB0 = mm(Pm, cB0r, 0.0);         // every column: P b0
-                const double PB1 = mm(Pm, cB1r, 0.0);         // every column: P b1
-                const double re00 = mm(cB0r, PB0, MT.R[0] + in[t].db0);   // every entry: (R + Db + B'PB)_00
-                const double re10 = mm(cB1r, PB0, MT.R[2]);
-                const double re11 = mm(cB1r, PB1, MT.R[3] + in[t].db1);
-                const double apT = mm(cA, T, cQ + in[t].Wt);  // Qbar_t + W_t + A'(P A)
-                const double app = mm(cA, pv, in[t].bxv);     // b^x_t + A'p
-                const double p0 = re00 > 0.0 ? re00 : 1e128;
-                const double det = fma(p0, re11, -(re10 * re10));   // p0 p1
-                const double r0 = frcp(p0);
-                const double rd = frcp(det > 0.0 ? det : 1.0);
-                const double ip1 = det > 0.0 ? p0 * rd : 1e-128;    // 1/p1, p1 = re11 - re10^2/p0
-                const double l = re10 * r0;
-                const double drow = mr == 0 ? r0 : ip1;
-                const double Xl = fma(-l, cB0m1, cBp);              // [B 0 0] E'
-                const double Y = mm(Xl, T, 0.0);                    // rows 0-1: E B'PA
-                const double yg = mm(Xl, pv, fma(-l, in[t].bu01, in[t].buT));   // rows 0-1: E (b^u + B'p)
-                o[t].En = fma(-l, k10, kd);                         // E (2x2 block)
-                o[t].Z = Y * drow;
-                o[t].zg = yg * drow;
-                o[t].l = l;
-                o[t].drow = drow;
-                // P_t = Qbar_t + W_t + A'(P A) - F'K with F'K = Y'Z;  p_t = b^x_t + A'p - K'g, K'g = Y'zg
-                Pm = mm_na(Y, o[t].Z, apT);
-                pv = mm_na(Y, o[t].zg, app);
-            }
-            if (t + 1 < N) {   // the previous stage's gain, multiplier and factor, off the recursion's path
-                const int r = (t + 1) * REC;
-                recm[r + oK] = mm(o[t + 1].En, o[t + 1].Z, 0.0);       // rows 0-1: E'D E F = Re^{-1} F
-                recm[r + oKPt] = mm(o[t + 1].En, o[t + 1].zg, 0.0);    // rows 0-1: Re^{-1} g
-                recm[r + O_CH] = o[t + 1].l;
-                recm[r + oDrow] = o[t + 1].drow;
-            }
-            stage_fence();
-        }
-        wb();
-    };
-    // backward linear pass with the stored factor: kappa_t = Re_t^{-1}(b^u_t + B'p_{t+1}) in the
-    // factored form above, p_t = b^x_t + A'p_{t+1} - K_t'g_t
-    auto back_mm = [&]() __attribute__((always_inline)) {
-        wb();
-        const PassK pk = pass_consts();
-        const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
-        struct In { double buT, bu01, l, drow, K, bxv; };
-        In in[N];
-        double En[N], zg[N];
-        auto load = [&](int t) {
-            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
-            in[t].buT = recm[r + oBUt];
-            in[t].bu01 = recm[r + oBU1];
-            in[t].l = recm[r + O_CH];
-            in[t].drow = recm[r + oDrow];
-            in[t].K = recm[r + oK];
-            in[t].bxv = recm[rp + O_BX + mr];
-        };
-        double pv = recm[(N - 1) * REC + O_BX + mr];
-#pragma unroll
-        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) load(t);
-        stage_fence();
-#pragma unroll
-        for (int t = N - 1; t >= -1; --t) {
-            if (t - kPre >= 0) load(t - kPre);
-            if (t >= 0) {
-                const double l = in[t].l;
-                const double g = mm(cBp, pv, in[t].buT);
-                const double app = mm(cA, pv, in[t].bxv);
-                const double yg = mm(fma(-l, cB0m1, cBp), pv, fma(-l, in[t].bu01, in[t].buT));
-                En[t] = fma(-l, k10, kd);
-                if (t >= 1) pv = mm_na(in[t].K, g, app);
-                zg[t] = yg * in[t].drow;
-            }
-            if (t + 1 < N) recm[(t + 1) * REC + oKPt] = mm(En[t + 1], zg[t + 1], 0.0);
-            stage_fence();
-        }
-        wb();
-    };
-    // forward pass: v_t = kappa_t - K_t y_t -> rec[t][16..17]; y_{t+1} = A y_t + B v_t -> rec[t][12..15]
-    auto forward_mm = [&]() __attribute__((always_inline)) {
-        wb();
-        const PassK pk = pass_consts();
-        const double cAT = mm(cA, pk.cI, 0.0), cBpT = mm(cBp, pk.cI, 0.0);   // (A')^ and [B 0 0]'^
-        double KT[N], kp[N], y[N + 1], v[N];
-        y[0] = 0.0;
-#pragma unroll
-        for (int t = 0; t < N && t < kPre; ++t) {
-            KT[t] = recm[t * REC + oKT];
-            kp[t] = recm[t * REC + oKPt];
-        }
-        stage_fence();
-#pragma unroll
-        for (int t = 0; t <= N; ++t) {
-            if (t + kPre < N) {
-                KT[t + kPre] = recm[(t + kPre) * REC + oKT];
-                kp[t + kPre] = recm[(t + kPre) * REC + oKPt];
-            }
-            if (t < N) {
-                v[t] = mm_na(KT[t], y[t], kp[t]);              // rows 0-1: kappa - K y
-                const double ay = mm(cAT, y[t], 0.0);          // A y
-                y[t + 1] = mm(cBpT, v[t], ay);                 // + B v
-            }
-            if (t >= 1) {
-                recm[(t - 1) * REC + O_BX + mr] = y[t];
-                recm[(t - 1) * REC + oBUt] = v[t - 1];
-            }
-            stage_fence();
-        }
-        wb();
-    };
-
-    // Each group claims its next instance from the launch's counter (S.claim, one atomic per
-    // instance by the group's lane 0) at the first trip after finishing one, so the 4 groups
-    // of a wave never wait for the slowest instance and no group is left with a heavier static
-    // share at the end of the launch.  Without a counter: static stride over the grid.
-    const int64_t stride = (int64_t)gridDim.x * WPB * 4;
-    auto claim = [&]() -> int64_t {
-        unsigned v = 0;
-        if (j == 0) v = atomicAdd(S.claim, 1u);
-        return (int64_t)__shfl(v, lane & ~(G16 - 1), 64);
-    };
-    // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
-    const int64_t nlive = S.count ? (int64_t)*S.count : batch;
-    int64_t slot = S.claim ? claim() : ((int64_t)blockIdx.x * WPB + wave) * 4 + g;
-    bool live = slot < nlive;   // the group has an instance to work on
-    // slot -> row: the caller's list, the hand-off record (polish launch), or the slot itself
-    auto row_of = [&](int64_t sl, bool lv) -> int64_t {
-        if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(lst0 + sl) * kRicRecWords + kRicRecRow] : sl;
-        else return lv && S.index ? (int64_t)S.index[sl] : sl;
-    };
-    int64_t inst = row_of(slot, live);
-    bool fresh = true;          // ... that still needs its initial point
-    double s_[RS], z_[RS];
-    double xs[2][4];
-    double bnorm = 1.0, qnorm = 1.0;
-    int it = 0, npol = 0;   // iterations; polish points passed over (pipeline rounds > 0)
-    bool polish_failed = false;
-    // Polish correction (shared-model kernels): when the acceptance test rejects the first attempt at a polish
-    // point and names rows to drop (active, negative multiplier) or to add (inactive, violated), the group's
-    // next trip polishes again on that corrected set (act_next: the set, bit 31 = such a trip is due); a second
-    // rejection stands.
-    unsigned act_next = 0;
-    // write the result of the current instance and move the group to its next one
-    auto finish = [&](int st, bool zero_u, bool write = true) {
-        if (write) {
-#pragma unroll
-            for (int sg = 0; sg < 2; ++sg)
-                if (own[sg]) {
-                    const int t = kseg[sg] - 1;
-                    u_out[inst * ld_u + 2 * t] = zero_u ? 0.0 : BX(F_U, sg, 0);
-                    u_out[inst * ld_u + 2 * t + 1] = zero_u ? 0.0 : BX(F_U, sg, 1);
-                }
-            if (j == 0) {
-                status_out[inst] = st;
-                if (iters_out) iters_out[inst] = it;
-            }
-        }
-        slot = S.claim ? claim() : slot + stride;
-        live = slot < nlive;
-        inst = row_of(slot, live);
-        fresh = true;
-    };
-    RT_DECL
-    while (__any(live)) {
-        bool active = live;
-        RT_MARK(11);
-        if (live && fresh) {
-            fresh = false;
-            if constexpr (!HET) {   // slot 11 of every record is the matrix-core passes' source of structural zeros
-                for (int t = j; t < N; t += G16) rec[t * REC + O_ZERO] = 0.0;
-            }
-            // this instance's data (HET) / the launch's problem
-            const double *Ipw = P.pre_w0, *IpE = P.pre_E, *Irw = P.r_w0, *IrE = P.r_E, *Ihq = P.hq;
-            const double *IpEd = P.pre_Ed, *IrEd = P.r_Ed, *Igoal = P.goal;
-            // The problem's data never changes inside the instance loop, and the compiler would hoist
-            // the loads below out of it -- dozens of registers of copies held for the whole kernel,
-            // which pushes row state out to scratch memory.  Passing the pointers through an empty asm
-            // makes them opaque, so the loads stay here.
-            asm volatile("" : "+s"(Ipw), "+s"(IpE), "+s"(Irw), "+s"(IrE), "+s"(Ihq), "+s"(IpEd), "+s"(IrEd), "+s"(Igoal));
-            int ji = j;   // likewise the lane's index into them (per-slot address offsets would be kept otherwise)
-            asm volatile("" : "+v"(ji));
-            if constexpr (HET) {
-                hinst = inst;
-#pragma unroll
-                for (int e = 0; e < 16; ++e) M.A[e] = P.het_A[inst * 16 + e];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) M.B[e] = P.het_B[inst * 8 + e];
-                Ipw += inst * P.het_sRow;
-                IpE += inst * P.het_sRow * NX;
-                Irw = P.het_ric_w0 + inst * (RS * G16);
-                IrE = P.het_ric_E + inst * (RS * G16) * NX;
-                Ihq += inst * P.het_sHq;
-            }
-            double xv0[NX], xr[NX];
-#pragma unroll
-            for (int k = 0; k < NX; ++k) {
-                if constexpr (MODE == 2)
-                    xv0[k] = reinterpret_cast<const double*>(W.pend_rec + (lst0 + slot) * kRicRecWords + kRicRecX0)[k];
-                else
-                    xv0[k] = x0[inst * NX + k];
-                xr[k] = xref ? xref[inst * NX + k] : Igoal[k];
-            }
-            // x0-only rows (G_r = 0): preconditions
-            const double dd = S.dist ? S.dist[inst] : 0.0;   // disturbance estimate (w -= Ed d)
-            double bad = 0.0;
-            if constexpr (MODE != 2)   // (handed-off instances have passed this test)
-            for (int r = ji; r < P.npre; r += G16) {
-                double v = Ipw[r];
-#pragma unroll
-                for (int k = 0; k < NX; ++k) v -= IpE[r * NX + k] * xv0[k];
-                if (IpEd) v -= IpEd[r] * dd;
-                bad = v < -PRE_TOL ? 1.0 : bad;
-            }
-            it = 0;
-            npol = 0;
-            polish_failed = false;
-            if constexpr (!HET) act_next = 0;
-            if (row_max(bad) > 0.0) {
-                finish(CARMPC_PRIMAL_INFEASIBLE, true);
-                active = false;
-            } else {
-                // per-slot w, q and box of the owned inputs, initial point
-                double bn = 0.0, qn = 0.0, u0n = 0.0;
-#pragma unroll
-                for (int s = 0; s < RS; ++s) {
-                    double v = 0.0;
-                    if (valid(s)) {
-                        const int e = s * G16 + ji;
-                        v = Irw[e];
-#pragma unroll
-                        for (int k = 0; k < NX; ++k) v -= IrE[e * NX + k] * xv0[k];
-                        if (IrEd) v -= IrEd[e] * dd;
-                    }
-                    wv.w[s][lane] = valid(s) ? v : 1.0;
-                    bn = fmax(bn, fabs(v));
-                }
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg) {
-                    const int t = kseg[sg] - 1;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int i = 2 * t + c;
-                        double q = 0.0;
-#pragma unroll
-                        for (int k = 0; k < NX; ++k) q = fma(Ihq[i * NX + k], xv0[k] - xr[k], q);
-                        const double lb = sh.lb[i], ub = sh.ub[i];
-                        const bool bx = own[sg] && boxed;
-                        const double u0 = bx ? fmin(fmax(0.0, lb), ub) : 0.0;
-                        BX(F_Q, sg, c) = own[sg] ? q : 0.0;
-                        BX(F_U, sg, c) = u0;
-                        const double su0 = fmax(ub - u0, kSFloor), sl0 = fmax(u0 - lb, kSFloor);
-                        BX(F_SU, sg, c) = bx ? su0 : 1.0;
-                        BX(F_SL, sg, c) = bx ? sl0 : 1.0;
-                        BX(F_ZU, sg, c) = bx ? 1.0 : 0.0;
-                        BX(F_ZL, sg, c) = bx ? 1.0 : 0.0;
-                        bn = bx ? fmax(bn, fmax(fabs(lb), fabs(ub))) : bn;
-                        qn = fmax(qn, own[sg] ? fabs(q) : 0.0);
-                        u0n = fmax(u0n, fabs(u0));
-                    }
-                }
-                // multipliers on the central path: z = mu0 / s with mu0 following the size of the linear term
-                double mu0 = 0.0;
-                if constexpr (!HET && MODE != 2) {
-                    if (kMu0 > 0.0) {
-                        const double qrel = kQInv * row_max(qn);
-                        mu0 = fmin(kMu0, fmax(kMuMin, qrel * qrel));
-#pragma unroll
-                        for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                            for (int c = 0; c < 2; ++c)
-                                if (own[sg] && boxed) {
-                                    BX(F_ZU, sg, c) = mu0 / BX(F_SU, sg, c);
-                                    BX(F_ZL, sg, c) = mu0 / BX(F_SL, sg, c);
-                                }
-                    }
-                }
-                if constexpr (MODE != 2) {   // the polish starts from the active set alone
-                // xs = S u0 (u0 = clip(0, lb, ub); zero whenever the box contains 0)
-                if (row_max(u0n) > 0.0) {
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-                        if (own[sg]) wr2((kseg[sg] - 1) * REC + O_BU, BX(F_U, sg, 0), BX(F_U, sg, 1));
-                    rollout();
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg) rd4((kseg[sg] - 1) * REC + O_BX, xs[sg]);
-                } else {
-#pragma unroll
-                    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) xs[sg][a] = 0.0;
-                }
-#pragma unroll
-                for (int s = 0; s < RS; ++s) {
-                    const int sg = s / RSEG;
-                    double c[4];
-                    cf(s, c);
-                    const double s0 = fmax(wv.w[s][lane] - dot4(c, xs[sg]), kSFloor);
-                    s_[s] = valid(s) ? s0 : 1.0;
-                    z_[s] = valid(s) ? (mu0 > 0.0 ? mu0 / s0 : 1.0) : 0.0;
-                }
-                }
-                bnorm = 1.0 + row_max(bn);
-                qnorm = 1.0 + row_max(qn);
-            }
-        }
-        RT_MARK(0);
-        if (!__any(active)) continue;
-        {
-            // ================= residuals (R1 + B1) =================
-            double mu = 0.0, rpn = 0.0, gun = 0.0, umax = 0.0, wz = 0.0, wzabs = 0.0;
-            double lo = 0.0, scf = 0.0;
-            bool polish = false;
-            // polish: the active set (rows with s < z) as a bit per slot, fixed when the polish factorizes;
-            // the polish loops test it instead of reading s and z (which they leave alone)
-            // (shared-model kernels: bits 16.. hold the box rows of the lane's inputs, upper and lower bound of
-            // input (sg, c) at 16 + 4 sg + 2 c and the bit above; per-instance kernels compare slack and multiplier)
-            unsigned actm = 0;
-#define RIC_REPOL (!HET && (act_next >> 31) != 0)   // this trip is the second attempt of a polish
-            if constexpr (!HET) {
-                if (RIC_REPOL) actm = act_next & 0xFFFFFFu;
-            }
-            auto act = [&](int s) { return ((actm >> s) & 1u) != 0; };
-            auto box_bit = [](int sg, int c, int lower) { return 16 + (sg * 2 + c) * 2 + lower; };
-            auto act_ub = [&](int sg, int c) {
-                if constexpr (HET) return boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c);
-                else return ((actm >> box_bit(sg, c, 0)) & 1u) != 0;
-            };
-            auto act_lb = [&](int sg, int c) {
-                if constexpr (HET) return boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c);
-                else return ((actm >> box_bit(sg, c, 1)) & 1u) != 0;
-            };
-            if (MODE != 2 && active) {
-                double lz[2][4], musum = -0.0;
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) lz[sg][a] = -0.0;
-                FOR_SLOTS_BEGIN
-                    const double w = in.w;
-                    const double gu = dot4(c, xs[sg]);
-                    const double rp = gu + s_[s] - w;
-                    rpn = fmax(rpn, fabs(rp));
-                    gun = fmax(gun, fabs(gu));
-                    musum = fma(s_[s], z_[s], musum);
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) lz[sg][a] = fma(z_[s], c[a], lz[sg][a]);
-                    wz = fma(w, z_[s], wz);
-                    wzabs = fma(fabs(w), z_[s], wzabs);
-                FOR_SLOTS_END
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int i = 2 * (kseg[sg] - 1) + c;
-                        if (own[sg] && boxed) {
-                            const double rpu = BX(F_U, sg, c) + BX(F_SU, sg, c) - sh.ub[i];
-                            const double rpl = -BX(F_U, sg, c) + BX(F_SL, sg, c) + sh.lb[i];
-                            rpn = fmax(rpn, fmax(fabs(rpu), fabs(rpl)));
-                            musum = fma(BX(F_SU, sg, c), BX(F_ZU, sg, c), fma(BX(F_SL, sg, c), BX(F_ZL, sg, c), musum));
-                            umax = fmax(umax, fabs(BX(F_U, sg, c)));
-                        }
-                    }
-                // stage-N sum of lamZ, owners write lamZ_k [0..3], lamH_k = Qbar_k xs_k [4..7]
-                double pn[4];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) pn[a] = row_sum((isN[0] ? lz[0][a] : 0.0) + (isN[1] ? lz[1][a] : 0.0));
-                wb();
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg)
-                    if (own[sg]) {
-                        double v[4], h[4] = {-0.0, -0.0, -0.0, -0.0};
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) v[a] = isN[sg] ? pn[a] : lz[sg][a];
-                        add_qbar(kseg[sg] == N, xs[sg], h, 1.0);
-                        wr4((kseg[sg] - 1) * REC + 0, v);
-                        wr4((kseg[sg] - 1) * REC + 4, h);
-                    }
-                RT_MARK(1);
-                mu = row_sum(musum) * inv_m;
-                rpn = row_max(rpn);
-                gun = row_max(gun);
-                umax = row_max(umax);
-                wz = row_sum(wz);
-                wzabs = row_sum(wzabs);
-            }
-            // B1 (per-instance models): psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1},
-            // redundantly in the 16 lanes of the group
-            auto adjoint_scalar = [&]() {
-                wb();
-                    double pz[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};
-                    double lzv[4], lhv[4];
-                    rd4((N - 1) * REC + 0, lzv);
-                    rd4((N - 1) * REC + 4, lhv);
-#pragma unroll kUnrollAdj
-                    for (int t = N - 1; t >= 0; --t) {
-                        const int r = t * REC;
-                        double nlz[4], nlh[4];
-                        rd4((t >= 1 ? r - REC : 0), nlz);
-                        rd4((t >= 1 ? r - REC : 0) + 4, nlh);
-                        double nz[4], nh[4];
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) {
-                            double az = lzv[a], ah = lhv[a];
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) {
-                                az = M.A_(c, a, pz[c], az);
-                                ah = M.A_(c, a, ph[c], ah);
-                            }
-                            nz[a] = az;
-                            nh[a] = ah;
-                        }
-                        double gz[2], hs[2];
-#pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            double az = -0.0, ah = -0.0;
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) {
-                                pz[a] = nz[a];
-                                ph[a] = nh[a];
-                                az = M.B_(a, c, nz[a], az);
-                                ah = M.B_(a, c, nh[a], ah);
-                            }
-                            gz[c] = az;
-                            hs[c] = ah;
-                            const double lb = sh.lb[2 * t + c], ub = sh.ub[2 * t + c];
-                            lo += fmin(az * lb, az * ub);
-                            scf = fma(fabs(az), fmax(fabs(lb), fabs(ub)), scf);
-                        }
-                        if (RIC_WRITER) {
-                            wr2(r + 12, gz[0], gz[1]);
-                            wr2(r + 14, hs[0], hs[1]);
-                        }
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) { lzv[a] = nlz[a]; lhv[a] = nlh[a]; }
-                    }
-                wb();
-            };
-            // B1: psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1}
-            if constexpr (HET) {
-                if (active) adjoint_scalar();
-            } else if constexpr (MODE != 2) {
-                adjoint_mm();
-            }
-            if (MODE != 2 && active) {
-                RT_MARK(2);
-                double rdn = 0.0, hun = 0.0, gzn = 0.0;
-#pragma unroll
-                for (int sg = 0; sg < 2; ++sg) {
-                    const int r = (kseg[sg] - 1) * REC;
-                    double gz0, gz1, hs0, hs1;
-                    rd2(r + 12, gz0, gz1);
-                    rd2(r + 14, hs0, hs1);
-                    const double gzv[2] = {gz0, gz1}, hsv[2] = {hs0, hs1};
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        if constexpr (!HET) {   // box-Farkas sums over the owned inputs (summed over the group below)
-                            const double lb = sh.lb[2 * (kseg[sg] - 1) + c], ub = sh.ub[2 * (kseg[sg] - 1) + c];
-                            if (own[sg]) {
-                                lo += fmin(gzv[c] * lb, gzv[c] * ub);
-                                scf = fma(fabs(gzv[c]), fmax(fabs(lb), fabs(ub)), scf);
-                            }
-                        }
-                        const double hu = hsv[c] + M.Rmul(c, BX(F_U, sg, 0), BX(F_U, sg, 1));
-                        const double gzb = gzv[c] + (boxed ? BX(F_ZU, sg, c) - BX(F_ZL, sg, c) : 0.0);
-                        const double rd = hu + BX(F_Q, sg, c) + gzb;
-                        BX(F_RD, sg, c) = own[sg] ? rd : 0.0;
-                        if (own[sg]) {
-                            rdn = fmax(rdn, fabs(rd));
-                            hun = fmax(hun, fabs(hu));
-                            gzn = fmax(gzn, fabs(gzb));
-                        }
-                    }
-                }
-                rdn = row_max(rdn);
-                hun = row_max(hun);
-                gzn = row_max(gzn);
-                if constexpr (!HET) {
-                    lo = row_sum(lo);
-                    scf = row_sum(scf);
-                }
-                const double pscale = fmax(bnorm, 1.0 + fmax(gun, umax));
-                const double dscale = fmax(qnorm, 1.0 + fmax(hun, gzn));
-                int done = -1;
-                if (!isfinite(mu) || !isfinite(rdn)) {
-                    done = CARMPC_NUMERICAL;
-                } else {
-                    const bool res_ok = rpn <= S.tol * pscale && rdn <= S.tol * dscale;
-                    const bool last = it >= S.max_iter;
-                    const double ptol = HET ? S.tol : fmax(POLISH_RES, S.tol);
-                    const bool pres_ok = rpn <= ptol * pscale && rdn <= ptol * dscale;
-                    polish = !polish_failed && ((pres_ok && mu <= (HET ? POLISH_MU_CONSERVATIVE : POLISH_MU)) || last);
-                    if constexpr (MODE != 2) {
-                        // round r of the pipeline (the single kernel after the last round included): the
-                        // instance's first r polishes are known to be rejected -- that is why it is here;
-                        // pass them over the way the single kernel carries on after a rejection: same
-                        // iterate, no polish until a step has been taken
-                        if (W.cnt && polish && npol < W.round) {
-                            ++npol;
-                            polish = false;
-                        }
-                    }
-                    if (!polish) {
-                        if (last) done = CARMPC_MAX_ITER;
-                        else if (res_ok && mu <= S.tol_mu) done = CARMPC_OPTIMAL;
-                        else if (p > 0 && lo - wz > 1e-12 * (scf + wzabs)) done = CARMPC_PRIMAL_INFEASIBLE;
-                    }
-                }
-                if (done >= 0) {
-                    finish(done, false);
-                    active = false;
-                    polish = false;
-                }
-                if constexpr (MODE == 1) {
-                    if (polish) {
-                        // hand the instance to the polish launch: active rows (s < z) and active box rows
-                        unsigned m = 0;
-                        for_used([&](const int s) __attribute__((always_inline)) { m |= (s_[s] < kAct * z_[s] ? 1u : 0u) << s; });
-#pragma unroll
-                        for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-                            for (int c = 0; c < 2; ++c)
-                                if (own[sg] && boxed) {
-                                    m |= (BX(F_SU, sg, c) < kAct * BX(F_ZU, sg, c) ? 1u : 0u) << box_bit(sg, c, 0);
-                                    m |= (BX(F_SL, sg, c) < kAct * BX(F_ZL, sg, c) ? 1u : 0u) << box_bit(sg, c, 1);
-                                }
-                        unsigned pos = 0;
-                        if (j == 0) pos = atomicAdd(W.cnt + kRicClaimStride * seg + 4 * W.round + 1, 1u);
-                        pos = __shfl(pos, lane & ~(G16 - 1), 64);
-                        uint32_t* hrec = W.pend_rec + (lst0 + pos) * kRicRecWords;
-                        hrec[j] = m;
-                        if (j < NX) reinterpret_cast<double*>(hrec + kRicRecX0)[j] = x0[inst * NX + j];
-                        if (j == 0) {
-                            hrec[kRicRecRow] = (uint32_t)inst;
-                            hrec[kRicRecIt] = (uint32_t)it;
-                        }
-                        finish(0, false, false);
-                        active = false;
-                        polish = false;
-                    }
-                }
-            }
-            if constexpr (MODE == 1) polish = false;   // (compile-time fact for the code below)
-            if constexpr (MODE == 2) {
-                // the hand-off record replaces residuals and decisions
-                polish = true;
-                if (active && !RIC_REPOL) {
-                    const uint32_t* hrec = W.pend_rec + (lst0 + slot) * kRicRecWords;
-                    actm = hrec[j];
-                    it = (int)hrec[kRicRecIt];
-                }
-            }
-            const bool any_polish = __any(polish);
-            RT_MARK(3);
-            if constexpr (HET) {
-                // per-instance models: both forms interleaved per group (flags per lane)
-                if (!__any(active)) continue;
-#define RIC_GO active
-#define RIC_POLISH polish
-#define RIC_ANY_POLISH any_polish
-#include "ipm_riccati_solve.inc"
-#undef RIC_GO
-#undef RIC_POLISH
-#undef RIC_ANY_POLISH
-            } else {
-                // Shared model: the rest of the trip exists in two compile-time forms, the interior-point step and the
-                // active-set polish.  The single kernel (MODE 0) runs the polish form first for the groups that polish
-                // in this trip, then the step form for the others: each form keeps only its own vectors live, where
-                // code that interleaves them per group keeps the union (and spilled to scratch).  MODE 1 / 2
-                // instantiate one form each.
-                auto solve_phase = [&](auto pol_c, bool go) __attribute__((always_inline)) {
-                    constexpr bool POL = decltype(pol_c)::value;
-                    if (!__any(go)) return;
-#define RIC_GO go
-#define RIC_POLISH POL
-#define RIC_ANY_POLISH POL
-#include "ipm_riccati_solve.inc"
-#undef RIC_GO
-#undef RIC_POLISH
-#undef RIC_ANY_POLISH
-                };
-                if constexpr (MODE != 1) {
-                    if (any_polish) solve_phase(std::true_type{}, active && polish);
-                }
-                if constexpr (MODE != 2) solve_phase(std::false_type{}, active && !polish);
-            }
-        }
-    }
-    RT_FLUSH();
-    }   // segments
-#undef RIC_REPOL
-}
-
-}  // namespace
+using namespace ric;
+namespace ric {
+RIC_INST(extern, false, 0)
+RIC_INST(extern, false, 1)
+RIC_INST(extern, false, 2)
+RIC_INST(extern, true, 0)
+}  // namespace ric
 
 bool riccati_supported_N(int N) { return N == 10 || N == 20; }
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
-// Wavefronts per workgroup by horizon: one workgroup per CU, so this is the number of waves that share a
-// CU's four SIMDs.  What limits it is LDS (the per-wave record, row and input state below).
-#ifndef CARMPC_RIC_WPB10
-#define CARMPC_RIC_WPB10 4
-#endif
-constexpr int ric_wpb(int N) { return N <= 10 ? CARMPC_RIC_WPB10 : 4; }
-template <int WPB, class Kern>
+template <int WPB, int LPQ, class Kern>
 hipError_t ric_launch(Kern kern, const RicSegs& T, const RicWork& W, int64_t total, const double* x0, const double* xref,
                       double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -1486,7 +27,7 @@ hipError_t ric_launch(Kern kern, const RicSegs& T, const RicWork& W, int64_t tot
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, WPB * 64, 0);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    const int64_t per_block = (int64_t)WPB * 4;
+    const int64_t per_block = (int64_t)WPB * (64 / LPQ);
     int64_t grid = std::min<int64_t>((int64_t)cus * per_cu, (total + per_block - 1) / per_block);
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WPB * 64), 0, stream, T, W, x0, xref, u_out, ld_u, status, iters, s);
@@ -1497,12 +38,13 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
                         double* u_out, int64_t ld_u, int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream,
                         int* unsupported) {
     const bool bike = T.P[0].ric == 2;
+    constexpr int LQ = ric_lpq(MODE, HET);
     if (HET && !bike) {   // per-instance models are always bicycle-structured (hetero.hip::linearize_kernel)
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
 #define RIC_GO(NN, MODEL) \
-    ric_launch<ric_wpb(NN)>(ipm_riccati_kernel<NN, ric_wpb(NN), MODEL, HET, MODE>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
+    ric_launch<ric_wpb(LQ), LQ>(ipm_riccati_kernel<NN, ric_wpb(LQ), MODEL, HET, MODE, LQ>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
     switch (T.P[0].N) {
         case 10: return bike ? RIC_GO(10, BicycleModel) : RIC_GO(10, DenseModel);
         case 20: return bike ? RIC_GO(20, BicycleModel) : RIC_GO(20, DenseModel);
@@ -1614,13 +156,18 @@ hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double*
 }  // namespace carmpc
 
 #ifdef CARMPC_PHASE_TIMING
-// Profiling build only: read (and optionally reset) the Riccati kernel's phase cycles.
+// Profiling build only: read (and optionally reset) the Riccati kernels' phase cycles, summed over the
+// translation units that instantiate the kernel.
+extern "C" int carmpc_debug_ric_cycles_m0(unsigned long long*, int);
+extern "C" int carmpc_debug_ric_cycles_m1(unsigned long long*, int);
+extern "C" int carmpc_debug_ric_cycles_m2(unsigned long long*, int);
+extern "C" int carmpc_debug_ric_cycles_het(unsigned long long*, int);
 extern "C" int carmpc_debug_ric_cycles(unsigned long long* out12, int reset) {
-    if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(carmpc_ric_cycles), sizeof(unsigned long long) * 12) != hipSuccess)
-        return -1;
-    if (reset) {
-        const unsigned long long z[12] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(carmpc_ric_cycles), z, sizeof(z)) != hipSuccess) return -1;
+    for (int i = 0; i < 12; ++i) out12[i] = 0;
+    for (auto fn : {carmpc_debug_ric_cycles_m0, carmpc_debug_ric_cycles_m1, carmpc_debug_ric_cycles_m2, carmpc_debug_ric_cycles_het}) {
+        unsigned long long part[12];
+        if (fn(part, reset) != 0) return -1;
+        for (int i = 0; i < 12; ++i) out12[i] += part[i];
     }
     return 0;
 }

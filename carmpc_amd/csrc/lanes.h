@@ -35,6 +35,29 @@ __device__ __forceinline__ double row_sum(double v) { return row_reduce<OpSum>(v
 __device__ __forceinline__ double row_max(double v) { return row_reduce<OpMax>(v); }
 __device__ __forceinline__ double row_min(double v) { return row_reduce<OpMin>(v); }
 
+// Exchange between the two 16-lane rows of a 32-lane half-wave (lane l <-> lane l ^ 16) with
+// v_permlane16_swap_b32 (gfx950: swaps the odd rows of its first operand with the even rows of its
+// second).  Given two copies of x, the first ends up holding the even row's value in both rows and
+// the second the odd row's value, so every lane of the pair combines (even, odd) in the same order:
+// the result is bitwise identical in both rows.
+template <class Op>
+__device__ __forceinline__ double pair_rows(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const double ev = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
+    const double od = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
+    return Op::f(ev, od);
+}
+// reduction over each group of LPQ lanes (LPQ = 16: one row; 32: two rows), result in every lane of the group
+template <int LPQ, class Op>
+__device__ __forceinline__ double grp_reduce(double v) {
+    static_assert(LPQ == 16 || LPQ == 32, "lanes per group");
+    if constexpr (LPQ == 32) v = pair_rows<Op>(v);
+    return row_reduce<Op>(v);
+}
+
 // Reciprocal: v_rcp_f64 is good to ~2^-25 (measured, tools/probe/rcp_probe.hip: max 2.5e8 ulp), so
 // one Newton step leaves <= 11 ulp (mean 0.6) -- enough for the scalings it is used for (z/s, step
 // ratios, pivots; the IPM's iterates are insensitive at that level and statuses and iteration
