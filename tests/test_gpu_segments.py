@@ -147,3 +147,49 @@ def test_pipeline_runs_that_do_not_start_at_instance_zero(gpu_available, case):
         ok = s1 == 0
         assert int(ok.sum()) > 0
         assert float((u1[ok] - u[sl, :p.n][ok]).abs().max()) <= 1e-12
+
+
+def test_host_pipeline_equals_resident_solve(gpu_available):
+    """States in host memory, results to host memory, copies overlapped with the solve chunk by chunk
+    (carmpc_amd.qp.HostPipeline): same statuses, iteration counts and inputs as one call on resident data,
+    for the default split and for chunks that cut through segments; repeated calls reuse the buffers."""
+    import torch
+    from carmpc_amd.qp import HostPipeline, solve_segments
+    probs = _problems()
+    counts = [30000, 41000, 27304]
+    offsets = np.concatenate([[0], np.cumsum(counts)])
+    B = int(offsets[-1])
+    X = _states(B, 33)
+    u0, s0, i0 = solve_segments(probs, offsets, torch.as_tensor(X).cuda())
+    torch.cuda.synchronize()
+    u0, s0, i0 = u0.cpu().numpy(), s0.cpu().numpy(), i0.cpu().numpy()
+    ok = s0 == 0
+    for chunks in (None, [50000, 20000, 28304]):
+        hp = HostPipeline(probs, offsets, chunks)
+        for rep in range(2):
+            u, st, it = hp.solve(X)
+            np.testing.assert_array_equal(st.numpy(), s0)
+            np.testing.assert_array_equal(it.numpy(), i0)
+            np.testing.assert_allclose(u.numpy()[ok], u0[ok], rtol=0, atol=1e-12)
+    # a sequence of batches with two in flight: batch k's results are those of batch k's states
+    hp = HostPipeline(probs, offsets, depth=2)
+    Xs = [X, X[::-1].copy(), X]                 # (the reversed batch puts other states under each problem)
+    refs = []
+    for Xk in Xs[:2]:
+        r = solve_segments(probs, offsets, torch.as_tensor(Xk).cuda())
+        torch.cuda.synchronize()
+        refs.append([t.cpu().numpy() for t in r])
+    refs.append(refs[0])
+    tickets = [hp.submit(Xs[0]), hp.submit(Xs[1])]
+    for k in range(3):
+        u, st, it = hp.wait(tickets[k])
+        np.testing.assert_array_equal(st.numpy(), refs[k][1])
+        np.testing.assert_array_equal(it.numpy(), refs[k][2])
+        okk = refs[k][1] == 0
+        np.testing.assert_allclose(u.numpy()[okk], refs[k][0][okk], rtol=0, atol=1e-12)
+        if k == 0:
+            tickets.append(hp.submit(Xs[2]))
+    u1, s1, i1 = probs[1].solve_host(X[:5000])
+    u2, s2, i2 = probs[1].solve(torch.as_tensor(X[:5000]).cuda())
+    np.testing.assert_array_equal(s1, s2.cpu().numpy())
+    np.testing.assert_allclose(u1[s1 == 0], u2.cpu().numpy()[s1 == 0], rtol=0, atol=1e-12)
