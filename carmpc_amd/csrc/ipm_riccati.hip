@@ -12,7 +12,12 @@ RIC_INST(extern, false, 2)
 RIC_INST(extern, true, 0)
 }  // namespace ric
 
-bool riccati_supported_N(int N) { return N == 10 || N == 20; }
+bool riccati_supported_N(int N) {
+#define RIC_IS_N(NN, ...) if (N == NN) return true;
+    RIC_FOR_EACH_N(RIC_IS_N, )
+#undef RIC_IS_N
+    return false;
+}
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
@@ -43,13 +48,15 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
         *unsupported = 1;
         return hipErrorInvalidValue;
     }
-#define RIC_GO(NN, MODEL) \
-    ric_launch<ric_wpb(LQ), LQ>(ipm_riccati_kernel<NN, ric_wpb(LQ), MODEL, HET, MODE, LQ>, T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream)
+#define RIC_GO(NN, MODEL)                                                                                              \
+    ric_launch<ric_wpb_for<NN, LQ>(), LQ>(ipm_riccati_kernel<NN, ric_wpb_for<NN, LQ>(), MODEL, HET, MODE, LQ>, T, W, total, x0, xref, \
+                                          u_out, ld_u, status, iters, s, stream)
+#define RIC_CASE(NN, ...) case NN: return bike ? RIC_GO(NN, BicycleModel) : RIC_GO(NN, DenseModel);
     switch (T.P[0].N) {
-        case 10: return bike ? RIC_GO(10, BicycleModel) : RIC_GO(10, DenseModel);
-        case 20: return bike ? RIC_GO(20, BicycleModel) : RIC_GO(20, DenseModel);
+        RIC_FOR_EACH_N(RIC_CASE, )
         default: *unsupported = 1; return hipErrorInvalidValue;
     }
+#undef RIC_CASE
 #undef RIC_GO
 }
 

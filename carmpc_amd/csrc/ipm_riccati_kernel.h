@@ -92,6 +92,10 @@ static __device__ unsigned long long carmpc_ric_cycles[12];
 #ifndef CARMPC_RIC_KPRE
 #define CARMPC_RIC_KPRE 1
 #endif
+// Scheduling barrier after every k-th row slot of the slot loops (0: none): bounds the live set of the loop.
+#ifndef CARMPC_RIC_SLOT_FENCE
+#define CARMPC_RIC_SLOT_FENCE 1
+#endif
 #ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
                                 // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
 #define CARMPC_RIC_UNROLL_HET 1
@@ -448,7 +452,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             const int qn = q + 1 < SL ? q + 1 : q;
             const SlotIn nxt = ld_slot((qn % NSG) * RSEG + (qn / NSG));
             body(s, cur);
-            __builtin_amdgcn_sched_barrier(0);
+            if (CARMPC_RIC_SLOT_FENCE != 0 && (q + 1) % (CARMPC_RIC_SLOT_FENCE != 0 ? CARMPC_RIC_SLOT_FENCE : 1) == 0)
+                __builtin_amdgcn_sched_barrier(0);
             cur = nxt;
         }
     };
@@ -1473,7 +1478,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             }
             const bool any_polish = __any(polish);
             RT_MARK(3);
-            if constexpr (HET) {
+#ifdef CARMPC_HET_TWO_FORM   // build-only switch for code inspection (tools/kernel_meta.py); never part of the product library
+            constexpr bool kInterleaved = false;
+#else
+            constexpr bool kInterleaved = HET;
+#endif
+            if constexpr (kInterleaved) {
                 // per-instance models: both forms interleaved per group (flags per lane)
                 if (!__any(active)) continue;
 #define RIC_GO active
@@ -1531,17 +1541,26 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 constexpr int ric_lpq(int mode, bool het) {
     return het ? 16 : mode == 1 ? CARMPC_RIC_LPQ_M1 : mode == 2 ? CARMPC_RIC_LPQ_M2 : CARMPC_RIC_LPQ_M0;
 }
-constexpr int ric_wpb(int lpq) { return 4 * lpq / 16; }
+// Wavefronts per workgroup: 16 QPs per workgroup where a CU's LDS (160 KB) holds them, fewer for longer horizons.
+template <int N, int LPQ>
+constexpr int ric_wpb_for() {
+    int w = 4 * LPQ / 16;
+    while (w > 1 && sizeof(RicShared<N>) + 16 + (size_t)w * sizeof(RicWave<N, LPQ>) > 160u * 1024u) --w;
+    return w;
+}
+// Horizons with a compiled instantiation (others run on the staged / dense kernels).
+#define RIC_FOR_EACH_N(X, ...) X(5, __VA_ARGS__) X(10, __VA_ARGS__) X(15, __VA_ARGS__) X(20, __VA_ARGS__) X(25, __VA_ARGS__)
 
 // The kernel is compiled in several translation units (ipm_riccati_m0 / _m1 / _m2 / _het.hip: one per launch
 // kind, each with the code-generation flags that suit it, carmpc_amd/build.py) and launched from
 // ipm_riccati.hip, which only declares the instantiations.
 #define RIC_KERNEL_ARGS RicSegs, RicWork, const double*, const double*, double*, int64_t, int32_t*, int32_t*, Settings
-#define RIC_INST(PREFIX, HET, MODE)                                                                                        \
-    PREFIX template __global__ void ipm_riccati_kernel<10, ric_wpb(ric_lpq(MODE, HET)), BicycleModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS); \
-    PREFIX template __global__ void ipm_riccati_kernel<10, ric_wpb(ric_lpq(MODE, HET)), DenseModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS);   \
-    PREFIX template __global__ void ipm_riccati_kernel<20, ric_wpb(ric_lpq(MODE, HET)), BicycleModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS); \
-    PREFIX template __global__ void ipm_riccati_kernel<20, ric_wpb(ric_lpq(MODE, HET)), DenseModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS);
+#define RIC_INST_N(NN, PREFIX, HET, MODE)                                                                              \
+    PREFIX template __global__ void                                                                                   \
+    ipm_riccati_kernel<NN, ric_wpb_for<NN, ric_lpq(MODE, HET)>(), BicycleModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS); \
+    PREFIX template __global__ void                                                                                   \
+    ipm_riccati_kernel<NN, ric_wpb_for<NN, ric_lpq(MODE, HET)>(), DenseModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS);
+#define RIC_INST(PREFIX, HET, MODE) RIC_FOR_EACH_N(RIC_INST_N, PREFIX, HET, MODE)
 
 }  // namespace ric
 }  // namespace carmpc

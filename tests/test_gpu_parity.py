@@ -95,11 +95,53 @@ def _settings(kernel):
     return SolverSettings(kernel=kernel)
 
 
+OTHER_HORIZONS = [("RoadEnv", 5), ("RoadOneCarEnv", 15), ("RoadMultipleCarsEnv", 25), ("RoadEnv", 25), ("RoadMultipleCarsEnv", 5)]
+
+
 def test_riccati_layout_selected(gpu_available):
-    """Every reference configuration (N in {10, 20}, nu = 2) gets the grouped Riccati kernel by default."""
-    for name, N in CONFIGS:
+    """Every reference configuration (N in {10, 20}, nu = 2) gets the grouped Riccati kernel by default, and so
+    do the other compiled horizons (5, 15, 25); a horizon without an instantiation falls back to the
+    wavefront-per-QP kernels."""
+    for name, N in CONFIGS + OTHER_HORIZONS:
         _, qp = _setup(name, N)
         assert qp.kernel == 7, (name, N)
+    _, qp = _setup("RoadEnv", 12)
+    assert qp.kernel in (1, 2)
+
+
+@pytest.mark.parametrize("name,N", OTHER_HORIZONS)
+def test_other_horizons_vs_c_oracle(gpu_available, name, N):
+    """Horizons other than the reference's default (configuration.py:16 is a free parameter of the
+    constructors, mpc.py:22-32): statuses and inputs against the C oracle, a sample against the certified
+    optimum, constraint and terminal-set feasibility on every optimal instance."""
+    import torch
+    from costs import OBJ_RTOL, objective_gap
+    from oracle.cpu import CpuProblem
+    from oracle import qp as oq
+    asm, qp = _setup(name, N)
+    rng = np.random.default_rng(100 + N)
+    B = 3000
+    X = np.stack([rng.uniform(asm.goal[0] - 1.3 * N, asm.goal[0], B), rng.uniform(-3, 3, B),
+                  rng.uniform(-np.pi / 8, np.pi / 8, B), rng.uniform(-1, 5, B)], axis=1)
+    u, st, it = qp.solve(torch.as_tensor(X).cuda())
+    u, st = u.cpu().numpy(), st.cpu().numpy()
+    uc, sc, ic = CpuProblem(asm).solve(X)
+    agree = st == sc
+    if not agree.all():
+        Gn, w0n, En, keep, pw, pE = oq.normalize_rows(asm.G, asm.w0, asm.E)
+        for i in np.where(~agree)[0]:
+            assert abs(oq.lp_margin(Gn, w0n - En @ X[i], asm.lb, asm.ub)) < 1e-7, (i, st[i], sc[i])
+    both = (st == 0) & (sc == 0)
+    assert both.sum() > B // 20 and (st >= 2).sum() == 0
+    assert np.abs(u[both] - uc[both]).max() <= U_TOL
+    tA, tb = asm.term_A[:, -4:], asm.term_b
+    for i in np.where(both)[0]:
+        assert _violation(asm, X[i], u[i]) <= VIOL_TOL
+        assert (tA @ (asm.T @ X[i] + asm.S @ u[i])[-4:] - tb).max() <= VIOL_TOL
+    for i in np.where(both)[0][:24]:
+        r = oq.solve_instance(asm, X[i])
+        assert r["certified"] and np.abs(u[i] - r["u_exact"]).max() <= U_TOL
+        assert objective_gap(asm, X[i], u[i], r["u_exact"]) <= OBJ_RTOL
 
 
 @pytest.mark.parametrize("kernel", KERNELS)

@@ -15,7 +15,8 @@ from test_zz_no_alloc import _call, _x0
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("env,N", [("RoadMultipleCarsEnv", 20), ("RoadEnv", 20), ("RoadOneCarEnv", 10)])
+@pytest.mark.parametrize("env,N", [("RoadMultipleCarsEnv", 20), ("RoadEnv", 20), ("RoadOneCarEnv", 10), ("RoadEnv", 15),
+                                   ("RoadMultipleCarsEnv", 25), ("RoadOneCarEnv", 5)])
 def test_pipeline_equals_single_kernel(gpu_available, env, N):
     import torch
     from oracle import assembly as oa
@@ -28,7 +29,9 @@ def test_pipeline_equals_single_kernel(gpu_available, env, N):
                    term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
     assert qp.kernel == 7
     B = 65536
-    X = torch.as_tensor(_x0(np.random.default_rng(11), asm.goal[0], B)).to(qp.device)
+    x = _x0(np.random.default_rng(11), asm.goal[0], B)
+    x[:, 0] = asm.goal[0] - (asm.goal[0] - x[:, 0]) * min(1.0, N / 20 * 1.05)      # (reachable within the horizon)
+    X = torch.as_tensor(x).to(qp.device)
     settings = SolverSettings()
     u1, st1, it1 = _call(lib.carmpc_solve_batch, qp, X, settings)            # pipeline
     u0, st0, it0 = _call(lib.carmpc_solve_batch_noalloc, qp, X, settings)    # single kernel
