@@ -661,12 +661,8 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     std::memcpy(P->A_host, d->A, sizeof(double) * NX * NX);
     DevProblem& D = P->dev;
     D.n = n; D.nv = nv; D.p = (int)qp.size(); D.npre = (int)pre.size(); D.ldg = nv + 2; D.N = N; D.nu = nu;
-    size_t lds = 0;
-    if (!dense_supported(nv, D.p, &lds)) {
-        delete P;
-        return fail(CARMPC_EUNSUPPORTED, "problem too large for the LDS-resident dense kernel (p=" +
-                                             std::to_string(D.p) + ", n=" + std::to_string(n) + ")");
-    }
+    // (a problem the dense kernel cannot hold in LDS is accepted when a stage-structured layout takes it, below)
+    const bool dense_ok = dense_supported(nv, D.p, nullptr);
     int32_t *dqp, *dpre, *stagep;
     double *Gp, *Ep, *w0p, *prew, *preE, *coefp;
     if ((e = upload(P, &dqp, qp.data(), qp.size())) != hipSuccess ||
@@ -704,6 +700,9 @@ int carmpc_problem_create(const carmpc_model_desc* d, carmpc_problem** out) {
     if (rc == CARMPC_OK) rc = stage_layout(P, d, qp, Phi, partner, &staged);
     bool ric = false;
     if (rc == CARMPC_OK) rc = riccati_layout(P, d, partner, &ric);
+    if (rc == CARMPC_OK && !dense_ok && !staged && !ric)
+        rc = fail(CARMPC_EUNSUPPORTED, "problem too large for the LDS-resident dense kernel (p=" + std::to_string(D.p) +
+                                           ", n=" + std::to_string(n) + ") and without a stage-structured layout");
     if (rc != CARMPC_OK) {
         delete P;
         return rc;
