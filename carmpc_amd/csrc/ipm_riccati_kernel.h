@@ -96,6 +96,9 @@ static __device__ unsigned long long carmpc_ric_cycles[12];
 #ifndef CARMPC_RIC_SLOT_FENCE
 #define CARMPC_RIC_SLOT_FENCE 1
 #endif
+#ifndef CARMPC_HET_LEGACY
+#define CARMPC_HET_LEGACY 0
+#endif
 #ifndef CARMPC_RIC_UNROLL_HET   // per-instance (HET) variant, both loop kinds: its A, B in registers
                                 // leave no room to unroll (hetero_bench 7.1M QP/s rolled, 6.4M at 5)
 #define CARMPC_RIC_UNROLL_HET 1
@@ -301,9 +304,14 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                                                                int32_t* __restrict__ status_all,
                                                                int32_t* __restrict__ iters_all, Settings S_all) {
     static_assert(!(HET && MODE != 0), "per-instance models run the single-kernel algorithm");
-    constexpr double kMu0 = HET ? 0.0 : CARMPC_INIT_MU0, kSFloor = HET ? 1.0 : CARMPC_INIT_SFLOOR;
-    constexpr int kPolRefine = HET ? POLISH_REFINE_CONSERVATIVE : POLISH_REFINE;
-    constexpr double kAct = HET ? 1.0 : POLISH_ACT;   // a row starts the polish active when s < kAct z
+    // Per-instance models run the algorithm and the matrix-core passes of the shared-model kernels (their stage
+    // matrices are reloaded per block whenever a group takes a new instance); HL selects their former variant --
+    // scalar stage passes with A, B in registers, one polish attempt behind the conservative gate, z = 1 start --
+    // in experiment builds (-DCARMPC_HET_LEGACY=1).
+    constexpr bool HL = HET && CARMPC_HET_LEGACY != 0;
+    constexpr double kMu0 = HL ? 0.0 : CARMPC_INIT_MU0, kSFloor = HL ? 1.0 : CARMPC_INIT_SFLOOR;
+    constexpr int kPolRefine = HL ? POLISH_REFINE_CONSERVATIVE : POLISH_REFINE;
+    constexpr double kAct = HL ? 1.0 : POLISH_ACT;   // a row starts the polish active when s < kAct z
     constexpr int kSolves = kPolRefine + 1 > 3 ? kPolRefine + 1 : 3;   // solves per trip: 3 of a step, kPolRefine + 1 of a polish
     constexpr double kMuMin = CARMPC_INIT_MU_MIN, kQInv = 1.0 / (CARMPC_INIT_Q_PER_VAR * 2 * N);
     constexpr int kUnroll = HET ? CARMPC_RIC_UNROLL_HET : CARMPC_RIC_UNROLL;
@@ -357,7 +365,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     if (kseg_i > 0) __syncthreads();   // every wave is done with the previous problem's tables
     if (batch <= 0) continue;
     const StageMats& MT = P.mats;
-    std::conditional_t<HET, MtH<SP>, const Mt<SP>> M{P.mats};
+    std::conditional_t<HL, MtH<SP>, const Mt<SP>> M{P.mats};
     int64_t hinst = 0;   // HET: the group's current instance (slice index)
     for (int i = threadIdx.x; i < kTab; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.r_coef[i * 4 + 0], P.r_coef[i * 4 + 1]);
@@ -641,28 +649,39 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     };
     // plain roll-out of v_t stored in rec[t][O_BU] (initial point): y -> rec[t][O_BX]
     auto rollout = [&]() {
-        wb();
-        double y[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll kUnroll
-        for (int t = 0; t < N; ++t) {
-            const int r = t * REC;
-            double v0, v1;
-            rd2(r + O_BU, v0, v1);
-            double ny[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                double acc = M.B_(a, 0, v0, -0.0);
-                acc = M.B_(a, 1, v1, acc);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc = M.A_(a, c, y[c], acc);
-                ny[a] = acc;
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) y[a] = ny[a];
+        auto run = [&](const auto& MM) __attribute__((always_inline)) {
             wb();
-            if (RIC_WRITER) wr4(r + O_BX, y);
+            double y[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int t = 0; t < N; ++t) {   // (rolled: this runs once per instance, and only when 0 lies outside the input box)
+                const int r = t * REC;
+                double v0, v1;
+                rd2(r + O_BU, v0, v1);
+                double ny[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) {
+                    double acc = MM.B_(a, 0, v0, -0.0);
+                    acc = MM.B_(a, 1, v1, acc);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc = MM.A_(a, c, y[c], acc);
+                    ny[a] = acc;
+                }
+#pragma unroll
+                for (int a = 0; a < 4; ++a) y[a] = ny[a];
+                wb();
+                if (RIC_WRITER) wr4(r + O_BX, y);
+            }
+            wb();
+        };
+        if constexpr (HET && !HL) {   // this instance's A, B (the only scalar stage loop of the per-instance kernels)
+            MtH<SP> Mh(P.mats);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) Mh.A[e] = P.het_A[hinst * 16 + e];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Mh.B[e] = P.het_B[hinst * 8 + e];
+            run(Mh);
+        } else {
+            run(M);
         }
-        wb();
     };
     // Riccati factorization with W_k, Db_t from rec, fused with the backward linear pass
     // of the first right-hand side (b^x, b^u in rec)   (oracle/riccati.py::riccati_factor)
@@ -833,6 +852,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     const int oKPt = m_top ? O_DB + mr : O_ZERO;               // kappa in rows 0-1
     const int oDrow = O_CH + (mr == 0 ? 1 : 2);                // 1/p0 in row 0, 1/p1 below
     double cA = 0.0, cBp = 0.0, cB0r = 0.0, cB1r = 0.0, cQ = 0.0, cPt = 0.0;
+    if constexpr (HET) cQ = MT.Q[mr * 4 + mc];   // (A, B, P of a per-instance model: reloaded when a group takes a new instance)
     if constexpr (!HET) {
         cA = MT.A[mr * 4 + mc];                       // A^
         cBp = m_left ? MT.B[mr * 2 + mc] : 0.0;       // [B 0 0]^
@@ -1084,9 +1104,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     while (__any(live)) {
         bool active = live;
         RT_MARK(11);
+        const bool setup_now = live && fresh;
         if (live && fresh) {
             fresh = false;
-            if constexpr (!HET) {   // slot 11 of every record is the matrix-core passes' source of structural zeros
+            if constexpr (!HL) {   // slot 11 of every record is the matrix-core passes' source of structural zeros
                 for (int t = j; t < N; t += GL) rec[t * REC + O_ZERO] = 0.0;
             }
             // this instance's data (HET) / the launch's problem
@@ -1102,10 +1123,12 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             const int ji = lzi % GL, tb = (LPQ == 32 ? ((lzi >> 4) & 1) * RSEG : 0) * G16 + (lzi & 15);
             if constexpr (HET) {
                 hinst = inst;
+                if constexpr (HL) {
 #pragma unroll
-                for (int e = 0; e < 16; ++e) M.A[e] = P.het_A[inst * 16 + e];
+                    for (int e = 0; e < 16; ++e) M.A[e] = P.het_A[inst * 16 + e];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) M.B[e] = P.het_B[inst * 8 + e];
+                    for (int e = 0; e < 8; ++e) M.B[e] = P.het_B[inst * 8 + e];
+                }
                 Ipw += inst * P.het_sRow;
                 IpE += inst * P.het_sRow * NX;
                 Irw = P.het_ric_w0 + inst * kTab;
@@ -1135,7 +1158,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             it = 0;
             npol = 0;
             polish_failed = false;
-            if constexpr (!HET) act_next = 0;
+            if constexpr (!HL) act_next = 0;
             if (row_max(bad) > 0.0) {
                 finish(CARMPC_PRIMAL_INFEASIBLE, true);
                 active = false;
@@ -1181,7 +1204,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 }
                 // multipliers on the central path: z = mu0 / s with mu0 following the size of the linear term
                 double mu0 = 0.0;
-                if constexpr (!HET && MODE != 2) {
+                if constexpr (!HL && MODE != 2) {
                     if (kMu0 > 0.0) {
                         const double qrel = kQInv * row_max(qn);
                         mu0 = fmin(kMu0, fmax(kMuMin, qrel * qrel));
@@ -1224,6 +1247,18 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 qnorm = 1.0 + row_max(qn);
             }
         }
+        if constexpr (HET && !HL) {
+            // a group has taken a new instance: the lanes of its matrix-core block (spread over all four rows of the
+            // wave) fetch that instance's A, B and terminal cost -- one matrix entry per lane, as for a shared model
+            if (__any(setup_now)) {
+                const int64_t hb = (int64_t)__shfl((int)hinst, (mb % NG) * GL, 64);
+                cA = P.het_A[hb * 16 + mr * 4 + mc];
+                cBp = m_left ? P.het_B[hb * 8 + mr * 2 + mc] : 0.0;
+                cB0r = P.het_B[hb * 8 + mr * 2];
+                cB1r = P.het_B[hb * 8 + mr * 2 + 1];
+                cPt = P.het_P[hb * 16 + (mr < mc ? mr : mc) * 4 + (mr < mc ? mc : mr)];
+            }
+        }
         RT_MARK(0);
         if (!__any(active)) continue;
         {
@@ -1236,18 +1271,18 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
             // (shared-model kernels: bits 16.. hold the box rows of the lane's inputs, upper and lower bound of
             // input (sg, c) at 16 + 4 sg + 2 c and the bit above; per-instance kernels compare slack and multiplier)
             unsigned actm = 0;
-#define RIC_REPOL (!HET && (act_next >> 31) != 0)   // this trip is the second attempt of a polish
-            if constexpr (!HET) {
+#define RIC_REPOL (!HL && (act_next >> 31) != 0)   // this trip is the second attempt of a polish
+            if constexpr (!HL) {
                 if (RIC_REPOL) actm = act_next & 0xFFFFFFu;
             }
             auto act = [&](int s) { return ((actm >> s) & 1u) != 0; };
             auto box_bit = [](int sg, int c, int lower) { return 16 + (sg * 2 + c) * 2 + lower; };
             auto act_ub = [&](int sg, int c) {
-                if constexpr (HET) return boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c);
+                if constexpr (HL) return boxed && BX(F_SU, sg, c) < BX(F_ZU, sg, c);
                 else return ((actm >> box_bit(sg, c, 0)) & 1u) != 0;
             };
             auto act_lb = [&](int sg, int c) {
-                if constexpr (HET) return boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c);
+                if constexpr (HL) return boxed && BX(F_SL, sg, c) < BX(F_ZL, sg, c);
                 else return ((actm >> box_bit(sg, c, 1)) & 1u) != 0;
             };
             if (MODE != 2 && active) {
@@ -1357,7 +1392,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 wb();
             };
             // B1: psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1}
-            if constexpr (HET) {
+            if constexpr (HL) {
                 if (active) adjoint_scalar();
             } else if constexpr (MODE != 2) {
                 adjoint_mm();
@@ -1374,7 +1409,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     const double gzv[2] = {gz0, gz1}, hsv[2] = {hs0, hs1};
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        if constexpr (!HET) {   // box-Farkas sums over the owned inputs (summed over the group below)
+                        if constexpr (!HL) {   // box-Farkas sums over the owned inputs (summed over the group below)
                             const double lb = sh.lb[2 * (kseg[sg] - 1) + c], ub = sh.ub[2 * (kseg[sg] - 1) + c];
                             if (own[sg]) {
                                 lo += fmin(gzv[c] * lb, gzv[c] * ub);
@@ -1395,7 +1430,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 rdn = row_max(rdn);
                 hun = row_max(hun);
                 gzn = row_max(gzn);
-                if constexpr (!HET) {
+                if constexpr (!HL) {
                     lo = row_sum(lo);
                     scf = row_sum(scf);
                 }
@@ -1407,9 +1442,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 } else {
                     const bool res_ok = rpn <= S.tol * pscale && rdn <= S.tol * dscale;
                     const bool last = it >= S.max_iter;
-                    const double ptol = HET ? S.tol : fmax(POLISH_RES, S.tol);
+                    const double ptol = HL ? S.tol : fmax(POLISH_RES, S.tol);
                     const bool pres_ok = rpn <= ptol * pscale && rdn <= ptol * dscale;
-                    polish = !polish_failed && ((pres_ok && mu <= (HET ? POLISH_MU_CONSERVATIVE : POLISH_MU)) || last);
+                    polish = !polish_failed && ((pres_ok && mu <= (HL ? POLISH_MU_CONSERVATIVE : POLISH_MU)) || last);
                     if constexpr (MODE != 2) {
                         // round r of the pipeline (the single kernel after the last round included): the
                         // instance's first r polishes are known to be rejected -- that is why it is here;

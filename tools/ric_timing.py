@@ -24,27 +24,33 @@ PHASES = ["init", "residual rows", "adjoint pass", "decisions", "factor rows", "
 
 
 def main():
-    kernel = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+    """Phase split per launch kind (translation unit) on the bench shard solved in one call (the three-launch form)."""
     dev = torch.device("cuda", 0)
     ctrls = bench.build_controllers(bench.ENVS, 20, dev)
     probs = [c.qp for c in ctrls]
     X, env, offsets = bench.sample_shard(0, bench.PER_GPU, [c.goal for c in ctrls])
     Xd = torch.as_tensor(X).to(dev)
-    fn = _native.load().carmpc_debug_ric_cycles
-    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    from carmpc_amd.qp import solve_segments
+    lib = _native.load()
     out = {}
-    for j, p in enumerate(probs):
-        sl = slice(int(offsets[j]), int(offsets[j + 1]))
-        buf = (ctypes.c_ulonglong * 12)()
-        p.solve(Xd[sl], settings=SolverSettings(kernel=kernel))
-        torch.cuda.synchronize()
-        fn(buf, 1)
-        p.solve(Xd[sl], settings=SolverSettings(kernel=kernel))
-        torch.cuda.synchronize()
-        fn(buf, 1)
+    units = {"m1": "iteration launch", "m2": "polish launch", "m0": "single kernel (retry launch)"}
+    fns = {}
+    for u in units:
+        fn = getattr(lib, "carmpc_debug_ric_cycles_" + u)
+        fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+        fns[u] = fn
+    buf = (ctypes.c_ulonglong * 12)()
+    solve_segments(probs, offsets, Xd)
+    torch.cuda.synchronize()
+    for u in units:
+        fns[u](buf, 1)
+    solve_segments(probs, offsets, Xd)
+    torch.cuda.synchronize()
+    for u, what in units.items():
+        fns[u](buf, 1)
         c = np.array(list(buf), dtype=np.float64)
-        out[bench.ENVS[j]] = {"share": {PHASES[i]: round(float(c[i] / c.sum()), 4) for i in range(12)},
-                              "total_cycles_all_waves": float(c.sum())}
+        out[what] = {"share": {PHASES[i]: round(float(c[i] / max(c.sum(), 1.0)), 4) for i in range(12)},
+                     "total_cycles_all_waves": float(c.sum())}
     print(json.dumps(out, indent=1))
 
 
