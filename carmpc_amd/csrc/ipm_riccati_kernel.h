@@ -1562,8 +1562,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 // four 16-lane groups (one wave per SIMD) or 8 wavefronts of two 32-lane groups (two waves per SIMD, 256
 // registers each).  Measured on the 131,072-instance mixed shard, QP/s: all launches with 16 lanes 19.9M; the
 // iteration launch with 32 lanes 21.0M; iteration and single kernel 21.4M; all three 21.6M (and only with all
-// three on one layout do the pipeline and the single kernel perform bit-identical arithmetic).  Per-instance
-// models keep 16 lanes (their A, B live in registers).
+// three on one layout do the pipeline and the single kernel perform bit-identical arithmetic).
 #ifndef CARMPC_RIC_LPQ_M1
 #define CARMPC_RIC_LPQ_M1 32
 #endif
@@ -1573,8 +1572,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 #ifndef CARMPC_RIC_LPQ_M0
 #define CARMPC_RIC_LPQ_M0 32
 #endif
+#ifndef CARMPC_RIC_LPQ_HET   // per-instance models: 14.9M QP/s with 16 lanes, 17.3M with 32 (131,072 instances)
+#define CARMPC_RIC_LPQ_HET 32
+#endif
 constexpr int ric_lpq(int mode, bool het) {
-    return het ? 16 : mode == 1 ? CARMPC_RIC_LPQ_M1 : mode == 2 ? CARMPC_RIC_LPQ_M2 : CARMPC_RIC_LPQ_M0;
+    return het ? CARMPC_RIC_LPQ_HET : mode == 1 ? CARMPC_RIC_LPQ_M1 : mode == 2 ? CARMPC_RIC_LPQ_M2 : CARMPC_RIC_LPQ_M0;
 }
 // Wavefronts per workgroup: 16 QPs per workgroup where a CU's LDS (160 KB) holds them, fewer for longer horizons.
 template <int N, int LPQ>
