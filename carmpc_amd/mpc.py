@@ -34,6 +34,45 @@ from .environments import BaseEnv
 from .simulator import CarTrailerDimension
 
 
+def _target_qp(Hd, M, rhs, A_in, b_in, tol=1e-9):
+    """min z'Hd z  s.t.  M z = rhs, A_in z <= b_in  for the handful of variables of a target selection
+    (mpc.py:413-437: x_ref and u_ref, Hd = blkdiag(Q, R) positive definite, so the minimiser is unique).
+    Exact active-set enumeration: for every set W of at most dim(null(M)) inequality rows the KKT system with
+    M z = rhs and the rows of W as equalities is solved; the feasible one with non-negative multipliers is the
+    optimum.  Returns z, or None when the constraints are inconsistent."""
+    from itertools import combinations
+    n = Hd.shape[0]
+    z_p, *_ = np.linalg.lstsq(M, rhs, rcond=None)
+    if np.abs(M @ z_p - rhs).max() > tol * (1.0 + np.abs(rhs).max()):
+        return None
+    _u, sv, vt = np.linalg.svd(M)
+    rank = int((sv > 1e-10 * max(sv.max(), 1.0)).sum())
+    Z = vt[rank:].T                                   # z = z_p + Z t
+    free = Z.shape[1]
+    best = None
+    for k in range(0, free + 1):
+        for W in combinations(range(A_in.shape[0]), k):
+            Aw = A_in[list(W)] @ Z if k else np.zeros((0, free))
+            if k and np.linalg.matrix_rank(Aw) < k:
+                continue
+            # stationarity in the reduced space: Z'Hd(z_p + Z t) + Aw' lam = 0, Aw t = b_w - A_w z_p
+            K = np.block([[Z.T @ Hd @ Z, Aw.T], [Aw, np.zeros((k, k))]]) if free else np.zeros((0, 0))
+            r = np.concatenate((-Z.T @ Hd @ z_p, (b_in[list(W)] - A_in[list(W)] @ z_p) if k else np.zeros(0)))
+            try:
+                sol = np.linalg.solve(K, r) if free else np.zeros(0)
+            except np.linalg.LinAlgError:
+                continue
+            z = z_p + Z @ sol[:free]
+            lam = sol[free:]
+            if (A_in @ z - b_in).max(initial=-np.inf) <= tol and (lam >= -tol).all():
+                val = z @ Hd @ z
+                if best is None or val < best[0]:
+                    best = (val, z)
+        if best is not None:
+            return best[1]
+    return None
+
+
 class OutsideTheRegionOfAttractionError(Exception):
     """The QP is infeasible: the initial state lies outside the region of attraction (mpc.py:17-18)."""
 
@@ -339,15 +378,26 @@ class MPCOutputFB(MPC):
         if self._ots is None:
             M = np.block([[np.eye(self.nx) - self.A, -self.B], [self.C, np.zeros((self.C.shape[0], self.nu))]])
             rhs = np.concatenate((np.zeros(self.nx), self.y_goal))
-            if np.linalg.matrix_rank(M) < self.nx + self.nu:
-                raise NotImplementedError("target selection with a non-unique equality solution")
-            xu, *_ = np.linalg.lstsq(M, rhs, rcond=None)
-            if np.abs(M @ xu - rhs).max() > 1e-9:
-                raise OutsideTheRegionOfAttractionError("no steady state reaches y_goal")
+            A_s, b_s = np.asarray(self.state_const_A, float), np.asarray(self.state_const_b, float)
+            if np.linalg.matrix_rank(M) == self.nx + self.nu:
+                # the feasible set of the equalities is one point: closed form, then the inequalities are a check
+                xu, *_ = np.linalg.lstsq(M, rhs, rcond=None)
+                if np.abs(M @ xu - rhs).max() > 1e-9:
+                    raise OutsideTheRegionOfAttractionError("no steady state reaches y_goal")
+                if (A_s @ xu[:self.nx] - b_s).max() > 1e-9 or np.any(xu[self.nx:] > self.input_upper + 1e-9) or \
+                        np.any(xu[self.nx:] < self.input_lower - 1e-9):
+                    raise OutsideTheRegionOfAttractionError("target violates the constraints")
+            else:
+                # a family of steady states reaches y_goal: the reference's QP picks the cheapest admissible one
+                A_in = np.block([[A_s, np.zeros((A_s.shape[0], self.nu))],
+                                 [np.zeros((self.nu, self.nx)), np.eye(self.nu)],
+                                 [np.zeros((self.nu, self.nx)), -np.eye(self.nu)]])
+                b_in = np.concatenate((b_s, self.input_upper, -np.asarray(self.input_lower)))
+                Hd = np.block([[self.Q, np.zeros((self.nx, self.nu))], [np.zeros((self.nu, self.nx)), self.R]])
+                xu = _target_qp(Hd, M, rhs, A_in, b_in)
+                if xu is None:
+                    raise OutsideTheRegionOfAttractionError("no admissible steady state reaches y_goal")
             x_ref, u_ref = xu[:self.nx], xu[self.nx:]
-            if (np.asarray(self.state_const_A) @ x_ref - np.asarray(self.state_const_b)).max() > 1e-9 or \
-                    np.any(u_ref > self.input_upper + 1e-9) or np.any(u_ref < self.input_lower - 1e-9):
-                raise OutsideTheRegionOfAttractionError("target violates the constraints")
             self._ots = (x_ref, u_ref)
         return self._ots
 

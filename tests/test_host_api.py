@@ -17,10 +17,11 @@ from oracle import assembly as oa
 def _ctrl(name, N, cls="MPCStateFB", **kw):
     from carmpc_amd import environments, mpc
     env = environments.ENVIRONMENTS[name]()
+    lin_state = kw.pop("lin_state", [0, 0, 0, 3])
     if cls == "MPCOutputFB":
-        return mpc.MPCOutputFB(0.2, N, [0, 0, 0, 3], [0, 0], [5, -1.5, 0, 0], env=env,
+        return mpc.MPCOutputFB(0.2, N, lin_state, [0, 0], [5, -1.5, 0, 0], env=env,
                                terminal_set_dir=TERMINAL_SETS, **kw)
-    return getattr(mpc, cls)(0.2, N, [0, 0, 0, 3], [0, 0], env=env, terminal_set_dir=TERMINAL_SETS, **kw)
+    return getattr(mpc, cls)(0.2, N, lin_state, [0, 0], env=env, terminal_set_dir=TERMINAL_SETS, **kw)
 
 
 @pytest.mark.parametrize("name,N", CONFIGS)
@@ -102,6 +103,54 @@ def test_output_fb_target_and_observer_host_forms():
     for i in range(len(g["y0"])):
         c.x_estimate, c.previous_u = g["x_estimate"][i].copy(), g["previous_u"][i].copy()
         np.testing.assert_allclose(c.luenberger_observer(g["y0"][i]), g["next"][i], rtol=0, atol=1e-13)
+
+
+def test_target_selection_with_a_family_of_steady_states():
+    """The reference's target-selection QP (mpc.py:413-437) when its equalities leave freedom: min x'Qx + u'Ru
+    over the admissible steady states that reach y_goal.  Checked against scipy's SLSQP on the same QP:
+    (a) the bicycle linearised at standstill (v = 0: heading and steering drop out of the equalities, the cost
+    sets them to zero), (b) a synthetic output map that measures only x and v, so that y, psi, delta are free
+    and a state row y >= 2 is active at the optimum."""
+    from scipy.optimize import minimize
+    from carmpc_amd import mpc as m
+
+    def slsqp(Hd, M, rhs, A_in, b_in):
+        # (SLSQP wants independent equality rows: the row space of M, with the consistent right-hand side)
+        _u, sv, vt = np.linalg.svd(M)
+        rank = int((sv > 1e-10 * sv.max()).sum())
+        z_p = np.linalg.lstsq(M, rhs, rcond=None)[0]
+        M, rhs = vt[:rank], vt[:rank] @ z_p
+        res = minimize(lambda z: z @ Hd @ z, np.zeros(6), jac=lambda z: 2 * Hd @ z, method="SLSQP",
+                       constraints=[{"type": "eq", "fun": lambda z: M @ z - rhs, "jac": lambda z: M},
+                                    {"type": "ineq", "fun": lambda z: b_in - A_in @ z, "jac": lambda z: -A_in}],
+                       options={"ftol": 1e-14, "maxiter": 500})
+        assert res.success
+        return res.x
+
+    c = _ctrl("RoadMultipleCarsEnv", 20, cls="MPCOutputFB")
+    Hd = np.block([[c.Q, np.zeros((4, 2))], [np.zeros((2, 4)), c.R]])
+    A_s, b_s = np.asarray(c.state_const_A, float), np.asarray(c.state_const_b, float)
+    A_in = np.block([[A_s, np.zeros((len(b_s), 2))], [np.zeros((2, 4)), np.eye(2)], [np.zeros((2, 4)), -np.eye(2)]])
+    b_in = np.concatenate((b_s, c.input_upper, -np.asarray(c.input_lower)))
+    # (a) standstill linearisation
+    c0 = _ctrl("RoadMultipleCarsEnv", 20, cls="MPCOutputFB", lin_state=[0, 0, 0, 0.0])
+    M0 = np.block([[np.eye(4) - c0.A, -c0.B], [c0.C, np.zeros((3, 2))]])
+    assert np.linalg.matrix_rank(M0) < 6
+    x_ref, u_ref = c0.optimal_target_selection()
+    ref = slsqp(Hd, M0, np.concatenate((np.zeros(4), c0.y_goal)), A_in, b_in)
+    np.testing.assert_allclose(np.concatenate((x_ref, u_ref)), ref, atol=1e-6)
+    np.testing.assert_allclose(x_ref, [30, 1.5, 0, 0], atol=1e-9)
+    # (b) outputs x and v only, with an extra admissible-state row y >= 2
+    C2 = np.array([[1.0, 0, 0, 0], [0, 0, 0, 1.0]])
+    M2 = np.block([[np.eye(4) - c.A, -c.B], [C2, np.zeros((2, 2))]])
+    rhs2 = np.concatenate((np.zeros(4), [30.0, 0.0]))
+    A2 = np.vstack((A_in, [[0, -1.0, 0, 0, 0, 0]]))
+    b2 = np.concatenate((b_in, [-2.0]))
+    z = m._target_qp(Hd, M2, rhs2, A2, b2)
+    np.testing.assert_allclose(z, slsqp(Hd, M2, rhs2, A2, b2), atol=1e-6)
+    assert abs(z[1] - 2.0) <= 1e-9 and abs(z[2]) <= 1e-9           # the row is active, the free heading is zero
+    # inconsistent constraints: y >= 2 against the road's y <= ... at a goal outside
+    assert m._target_qp(Hd, M2, rhs2, np.vstack((A2, [[0, 1.0, 0, 0, 0, 0]])), np.concatenate((b2, [1.0]))) is None
 
 
 def test_lqr_path():
