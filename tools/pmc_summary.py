@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--counters", nargs="*", default=[])
-    ap.add_argument("--match", default="carmpc::ipm_")
+    ap.add_argument("--match", default="ipm_")
     ap.add_argument("--segments", type=int, default=3)
     ap.add_argument("--key", required=True)
     ap.add_argument("--per-gpu", type=int, default=131072)
