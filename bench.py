@@ -386,7 +386,7 @@ def run(args, backend_cls=None) -> dict | None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall_max = float(t.item())
     kern_ms = be.device_ms(evs)
-    e2e = be.e2e_qps(X)
+    e2e = None if args.no_e2e else be.e2e_qps(X)
     st_np, it_np = be.results()
     if rank != 0:
         if dist is not None:
@@ -518,6 +518,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=131072,
                     help="instances of rank 0's shard timed on the host (all cores; an eighth of them on one thread)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive runs (profiles of the timed steps alone)")
     ap.add_argument("--per-problem-launches", action="store_true",
                     help="one carmpc_solve_batch launch per environment instead of one carmpc_solve_segments call")
     ap.add_argument("--kernel", type=int, default=0, help="carmpc_settings.kernel (0 auto, 1 dense, 2 staged, 7 riccati)")
