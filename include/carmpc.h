@@ -92,8 +92,8 @@ typedef struct {
                           with nu=2 and a compiled N), 3 = dense with 4 waves per
                           workgroup, 4-6 = staged variants of experiment builds only (rejected
                           with CARMPC_EUNSUPPORTED otherwise), 7 = grouped stage-form
-                          (Riccati) kernel, 16 lanes per QP (assembled, nu=2, N in
-                          {10,20}, <= 8 rows per stage) */
+                          (Riccati) kernel, 32 lanes per QP (assembled, nu=2, N in
+                          {5,10,15,20,25}, <= 8 rows per stage) */
 } carmpc_settings;
 
 /* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged, 7 grouped Riccati. */
