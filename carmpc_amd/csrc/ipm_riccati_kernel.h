@@ -421,6 +421,19 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     auto row_sum = [](double v) __attribute__((always_inline)) { return grp_reduce<LPQ, OpSum>(v); };
     auto row_max = [](double v) __attribute__((always_inline)) { return grp_reduce<LPQ, OpMax>(v); };
     auto row_min = [](double v) __attribute__((always_inline)) { return grp_reduce<LPQ, OpMin>(v); };
+    // Totals over the rows of stage N, wanted by the owner of stage N alone.  With 32 lanes per QP and N >= 17 that
+    // owner (lane N - 1) and every overflow lane sit in the group's upper DPP row, the lower row contributes
+    // zeros: the 16-lane butterfly is the whole sum there (the lower row's lanes get a value nobody reads).
+    constexpr bool kStageNUpperRow = LPQ == 32 && N >= 17;
+    auto stageN_sum = [&](double v) __attribute__((always_inline)) {
+        if constexpr (kStageNUpperRow) return lanes::row_reduce<OpSum>(v);
+        else return grp_reduce<LPQ, OpSum>(v);
+    };
+    // ... two of them at a time (lanes.h: the second value rides in the lower row through the same butterfly)
+    auto stageN_sum2 = [&](double& a, double& b) __attribute__((always_inline)) {
+        if constexpr (kStageNUpperRow) upper_row_sum2(a, b);
+        else grp_reduce2<LPQ, OpSum>(a, b);
+    };
     // this lane's part of a stage-N total: the entries of its segments that belong to stage N
     auto stageN_part = [&](const auto& v, int e) __attribute__((always_inline)) {
         double t = isN[0] ? v[0][e] : 0.0;
@@ -538,7 +551,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 #pragma unroll
         for (int a = 0; a < 4; ++a) pn[a] = stageN_part(acc, a);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) pn[a] = row_sum(pn[a]);
+        for (int a = 0; a < 4; a += 2) stageN_sum2(pn[a], pn[a + 1]);
 #pragma unroll
         for (int sg = 0; sg < NSG; ++sg) {
             if (own[sg]) {
@@ -1319,7 +1332,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 // stage-N sum of lamZ, owners write lamZ_k [0..3], lamH_k = Qbar_k xs_k [4..7]
                 double pn[4];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) pn[a] = row_sum(stageN_part(lz, a));
+                for (int a = 0; a < 4; ++a) pn[a] = stageN_part(lz, a);
+#pragma unroll
+                for (int a = 0; a < 4; a += 2) stageN_sum2(pn[a], pn[a + 1]);
                 wb();
 #pragma unroll
                 for (int sg = 0; sg < NSG; ++sg)
@@ -1333,11 +1348,9 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                     }
                 RT_MARK(1);
                 mu = row_sum(musum) * inv_m;
-                rpn = row_max(rpn);
-                gun = row_max(gun);
-                umax = row_max(umax);
-                wz = row_sum(wz);
-                wzabs = row_sum(wzabs);
+                gun = fmax(gun, umax);   // (only their maximum is used)
+                grp_reduce2<LPQ, OpMax>(rpn, gun);
+                grp_reduce2<LPQ, OpSum>(wz, wzabs);
             }
             // B1 (per-instance models): psiZ_k = lamZ_k + A'psiZ_{k+1}, psiH likewise; gz_t = B'psiZ_{t+1},
             // redundantly in the 16 lanes of the group
@@ -1427,15 +1440,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         }
                     }
                 }
-                rdn = row_max(rdn);
-                hun = row_max(hun);
-                gzn = row_max(gzn);
-                if constexpr (!HL) {
-                    lo = row_sum(lo);
-                    scf = row_sum(scf);
-                }
-                const double pscale = fmax(bnorm, 1.0 + fmax(gun, umax));
-                const double dscale = fmax(qnorm, 1.0 + fmax(hun, gzn));
+                hun = fmax(hun, gzn);    // (only their maximum is used)
+                grp_reduce2<LPQ, OpMax>(rdn, hun);
+                if constexpr (!HL) grp_reduce2<LPQ, OpSum>(lo, scf);
+                const double pscale = fmax(bnorm, 1.0 + gun);
+                const double dscale = fmax(qnorm, 1.0 + hun);
                 int done = -1;
                 if (!isfinite(mu) || !isfinite(rdn)) {
                     done = CARMPC_NUMERICAL;

@@ -50,6 +50,44 @@ __device__ __forceinline__ double pair_rows(double v) {
     const double od = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
     return Op::f(ev, od);
 }
+// Two reductions over a 32-lane group for little more than the price of one: the lower row takes over `a` and the
+// upper row `b` (one swap: afterwards the first register holds the lower lane's value in both rows, the second the
+// upper lane's), one 16-lane butterfly then reduces `a` in the lower row and `b` in the upper row at the same
+// time, and a last swap hands each row the other's total.  Both results bitwise uniform over the 32 lanes.
+__device__ __forceinline__ void swap16(double& x, double& y) {   // rows of x: (x.even, y.even); of y: (x.odd, y.odd)
+    const unsigned long long bx = __builtin_bit_cast(unsigned long long, x), by = __builtin_bit_cast(unsigned long long, y);
+    const auto rl = __builtin_amdgcn_permlane16_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+    x = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
+    y = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
+}
+template <int LPQ, class Op>
+__device__ __forceinline__ void grp_reduce2(double& a, double& b) {
+    if constexpr (LPQ == 32) {
+        double x = a, y = b;
+        swap16(x, y);                       // x: (a_lower, b_lower), y: (a_upper, b_upper)  [even row, odd row]
+        double t = row_reduce<Op>(Op::f(x, y));
+        double u = t;
+        swap16(t, u);                       // t: total of a in both rows, u: total of b
+        a = t;
+        b = u;
+    } else {
+        a = row_reduce<Op>(a);
+        b = row_reduce<Op>(b);
+    }
+}
+// The same for two sums whose addends all sit in the UPPER row of each 32-lane group (the lower row's inputs are
+// ignored): b's addends move to the lower row, one butterfly, and the upper row gets b's total back.  Results valid
+// in the upper row only.
+__device__ __forceinline__ void upper_row_sum2(double& a, double& b) {
+    double x = b, y = a;
+    swap16(x, y);                           // y: (b_upper, a_upper)
+    y = row_reduce<OpSum>(y);               // lower row: total of b, upper row: total of a
+    double z = y;
+    swap16(z, y);                           // z.odd row = y.even row = total of b
+    a = y;                                  // (upper row: total of a)
+    b = z;
+}
 // reduction over each group of LPQ lanes (LPQ = 16: one row; 32: two rows), result in every lane of the group
 template <int LPQ, class Op>
 __device__ __forceinline__ double grp_reduce(double v) {
