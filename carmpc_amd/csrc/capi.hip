@@ -310,6 +310,8 @@ int stage_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vecto
 // to the owner's segment; stage-N rows (terminal set + state rows on x_N) fill the owner of
 // N first, then the "overflow" segments whose stage number exceeds N (least-filled first).
 // Slot e = (seg*8 + s)*16 + j.  Returns ok=false (kernel unavailable) when it does not fit.
+// (set while the template problem of a per-instance batch is created: its kernels read both segments, 32 lanes per QP)
+thread_local bool g_two_segments_only = false;
 int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vector<int32_t>& partner, bool* ok) {
     *ok = false;
     DevProblem& D = P->dev;
@@ -331,31 +333,44 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
         if (k < 1 || k > N) return CARMPC_OK;
         ++per_stage[k];
     }
-    int rseg = 1, n_over = 0;
-    for (int k = 1; k < N; ++k) rseg = std::max(rseg, per_stage[k]);
-    for (int s2 = 0; s2 < 2; ++s2)
-        for (int j2 = 0; j2 < 16; ++j2) n_over += (j2 + 1 + 16 * s2 > N) ? 1 : 0;
-    rseg = std::max(rseg, (per_stage[N] + n_over) / (n_over + 1));   // ceil(rows_N / (owner + overflow segments))
-    if (rseg > kRicSeg) return CARMPC_OK;
-    int cnt[2][16] = {};
-    std::vector<int32_t> slot_of(D.p, -1);
-    for (int r = 0; r < D.p; ++r) {
-        const int k = stage[r];
-        int sg = (k - 1) / 16, j = (k - 1) % 16;
-        if (cnt[sg][j] >= rseg) {
-            if (k != N) return CARMPC_OK;
-            int best = -1;
-            for (int s2 = 0; s2 < 2; ++s2)
-                for (int j2 = 0; j2 < 16; ++j2)
-                    if (j2 + 1 + 16 * s2 > N && cnt[s2][j2] < rseg && (best < 0 || cnt[s2][j2] < cnt[best / 16][best % 16]))
-                        best = s2 * 16 + j2;
-            if (best < 0) return CARMPC_OK;
-            sg = best / 16;
-            j = best % 16;
+    // Placement with `nsg` segments of 16 table lanes: stage k <= 16 nsg in segment (k - 1) / 16, lane (k - 1) % 16;
+    // segments whose stage number exceeds N take the stage-N rows that do not fit the owner.  One segment (short
+    // horizons) is tried first: the kernels then carry four QPs per wavefront instead of two.
+    std::vector<int32_t> slot_of;
+    int rseg = 0, rone = 0;
+    auto place = [&](int nsg) {
+        if (N > 16 * nsg) return false;
+        int rs = 1, n_over = 0;
+        for (int k = 1; k < N; ++k) rs = std::max(rs, per_stage[k]);
+        for (int s2 = 0; s2 < nsg; ++s2)
+            for (int j2 = 0; j2 < 16; ++j2) n_over += (j2 + 1 + 16 * s2 > N) ? 1 : 0;
+        rs = std::max(rs, (per_stage[N] + n_over) / (n_over + 1));   // ceil(rows_N / (owner + overflow segments))
+        if (rs > kRicSeg) return false;
+        int cnt[2][16] = {};
+        std::vector<int32_t> so(D.p, -1);
+        for (int r = 0; r < D.p; ++r) {
+            const int k = stage[r];
+            int sg = (k - 1) / 16, j = (k - 1) % 16;
+            if (cnt[sg][j] >= rs) {
+                if (k != N) return false;
+                int best = -1;
+                for (int s2 = 0; s2 < nsg; ++s2)
+                    for (int j2 = 0; j2 < 16; ++j2)
+                        if (j2 + 1 + 16 * s2 > N && cnt[s2][j2] < rs && (best < 0 || cnt[s2][j2] < cnt[best / 16][best % 16]))
+                            best = s2 * 16 + j2;
+                if (best < 0) return false;
+                sg = best / 16;
+                j = best % 16;
+            }
+            so[r] = ((sg * kRicSeg + cnt[sg][j]) * 16) + j;
+            ++cnt[sg][j];
         }
-        slot_of[r] = ((sg * kRicSeg + cnt[sg][j]) * 16) + j;
-        ++cnt[sg][j];
-    }
+        slot_of = so;
+        rseg = rs;
+        return true;
+    };
+    if (!g_two_segments_only && riccati_oneseg_N(N) && place(1)) rone = 1;
+    else if (!place(2)) return CARMPC_OK;
     const int ns = kRicSlots * kRicLanes;
     std::vector<double> sc((size_t)ns * NX, 0.0), sw(ns, 0.0), sE((size_t)ns * NX, 0.0);
     std::vector<int32_t> sv(ns, 0), sp(ns, -1);
@@ -408,6 +423,7 @@ int riccati_layout(carmpc_problem* P, const carmpc_model_desc* d, const std::vec
                       zero_outside(M.R, 2, 2, keepR, 2);
     D.ric = bike ? 2 : 1;
     D.rseg = rseg;
+    D.rone = rone;
     P->ric_slot = slot_of;
     *ok = true;
     return CARMPC_OK;
@@ -444,7 +460,9 @@ int hetero_riccati_template(carmpc_hetero* h, const carmpc_hetero_desc* d) {
     md.n_term_rows = d->n_term_rows; md.term_A = d->term_A; md.term_b = d->term_b;
     md.u_lower = d->u_lower; md.u_upper = d->u_upper; md.goal = d->goal;
     carmpc_problem* T = nullptr;
+    g_two_segments_only = true;
     const int rc = carmpc_problem_create(&md, &T);
+    g_two_segments_only = false;
     if (rc != CARMPC_OK) return rc;
     h->tmpl = T;
     if (T->dev.ric != 2 || T->ric_slot.size() != T->qp_rows.size()) return CARMPC_OK;   // no bicycle layout
@@ -832,7 +850,8 @@ int carmpc_solve_segments(const carmpc_problem* const* probs, int32_t nprobs, co
         size_t i1 = i + 1;
         if (ric_ok(live[i]))
             while (i1 < live.size() && i1 - i < (size_t)kRicMaxSeg && live[i1] == live[i1 - 1] + 1 && ric_ok(live[i1]) &&
-                   probs[live[i1]]->dev.N == probs[live[i]]->dev.N && probs[live[i1]]->dev.ric == probs[live[i]]->dev.ric)
+                   probs[live[i1]]->dev.N == probs[live[i]]->dev.N && probs[live[i1]]->dev.ric == probs[live[i]]->dev.ric &&
+                   probs[live[i1]]->dev.rone == probs[live[i]]->dev.rone)
                 ++i1;
         int unsupported = 0;
         hipError_t e = hipSuccess;

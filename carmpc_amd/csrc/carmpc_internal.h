@@ -69,6 +69,7 @@ struct DevProblem {
     // lane j owns stage j+1 (segment 0) and j+17 (segment 1); slot e = (seg*8 + s)*16 + j
     int32_t ric;              // layout present: 1 dense stage matrices, 2 bicycle sparsity
     int32_t rseg;             // slots per segment in use (every lane): the kernels skip the rest
+    int32_t rone;             // every row sits in segment 0 (horizons <= 16 whose rows fit 16 lanes x 8 slots)
     const double* r_coef;     // 256 x NX  normalised row coefficients c~ of each slot
     const double* r_w0;       // 256
     const double* r_E;        // 256 x NX
@@ -271,6 +272,7 @@ int dense_pick_nv(int n);
 // Grouped stage-form (Riccati) kernel (ipm_riccati.hip).
 constexpr int kRicLanes = 16, kRicSeg = 8, kRicSlots = 2 * kRicSeg;
 bool riccati_supported_N(int N);
+bool riccati_oneseg_N(int N);   // ... with the four-QPs-per-wave instantiation for rows that fit one slot segment
 hipError_t launch_riccati(const DevProblem& P, int64_t batch, const double* x0, const double* xref,
                           double* u_out, int64_t ld_u, int32_t* status, int32_t* iters,
                           const Settings& s, hipStream_t stream, int* unsupported, bool het = false);

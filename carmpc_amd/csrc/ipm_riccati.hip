@@ -10,6 +10,9 @@ RIC_INST(extern, false, 0)
 RIC_INST(extern, false, 1)
 RIC_INST(extern, false, 2)
 RIC_INST(extern, true, 0)
+RIC_INST_ONESEG(extern, 0)
+RIC_INST_ONESEG(extern, 1)
+RIC_INST_ONESEG(extern, 2)
 }  // namespace ric
 
 bool riccati_supported_N(int N) {
@@ -18,6 +21,9 @@ bool riccati_supported_N(int N) {
 #undef RIC_IS_N
     return false;
 }
+
+bool riccati_oneseg_N(int N) { return ric_has_oneseg(N); }
+constexpr int64_t kRicOneSegMin = 16384;
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
@@ -51,11 +57,29 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
 #define RIC_GO(NN, MODEL)                                                                                              \
     ric_launch<ric_wpb_for<NN, LQ>(), LQ>(ipm_riccati_kernel<NN, ric_wpb_for<NN, LQ>(), MODEL, HET, MODE, LQ>, T, W, total, x0, xref, \
                                           u_out, ld_u, status, iters, s, stream)
+#define RIC_GO1(NN, MODEL)                                                                                             \
+    ric_launch<ric_wpb_for<NN, 16, 1>(), 16>(ipm_riccati_kernel<NN, ric_wpb_for<NN, 16, 1>(), MODEL, false, MODE, 16, 1>, T, W, total, \
+                                             x0, xref, u_out, ld_u, status, iters, s, stream)
 #define RIC_CASE(NN, ...) case NN: return bike ? RIC_GO(NN, BicycleModel) : RIC_GO(NN, DenseModel);
+#define RIC_CASE1(NN, ...) case NN: return bike ? RIC_GO1(NN, BicycleModel) : RIC_GO1(NN, DenseModel);
+    if constexpr (!HET) {
+        // rows in the first slot segment alone (short horizons): four QPs per wavefront
+        // (from kRicOneSegMin instances on: a small batch spreads over twice the wavefronts, hence CUs, with two QPs per
+        // wave, and its time is the latency of one solve -- 4,096 instances at N = 10: 15.0M QP/s with two per wave,
+        // 13.7M with four; 65,536: 29.1M against 37.4M; 131,072: 32.7M against 43.3M)
+        if (T.P[0].rone && ric_has_oneseg(T.P[0].N) && total >= kRicOneSegMin) {
+            switch (T.P[0].N) {
+                RIC_FOR_EACH_N_ONESEG(RIC_CASE1, )
+                default: break;
+            }
+        }
+    }
     switch (T.P[0].N) {
         RIC_FOR_EACH_N(RIC_CASE, )
         default: *unsupported = 1; return hipErrorInvalidValue;
     }
+#undef RIC_CASE1
+#undef RIC_GO1
 #undef RIC_CASE
 #undef RIC_GO
 }
@@ -137,7 +161,7 @@ hipError_t launch_riccati_segs(const RicSegs& T, const double* x0, const double*
         return hipErrorInvalidValue;
     }
     for (int j = 0; j < nseg; ++j)
-        if (!T.P[j].ric || T.P[j].N != T.P[0].N || T.P[j].ric != T.P[0].ric) {
+        if (!T.P[j].ric || T.P[j].N != T.P[0].N || T.P[j].ric != T.P[0].ric || T.P[j].rone != T.P[0].rone) {
             *unsupported = 1;
             return hipErrorInvalidValue;
         }

@@ -184,9 +184,9 @@ struct RicShared {
 // per-input state of the owned inputs, one row of 12 fields x 2 components per input pair t
 // (row N: dummy row written by lanes whose segment owns no input)
 enum { F_U = 0, F_Q, F_SU, F_SL, F_ZU, F_ZL, F_RD, F_E1, F_E2, F_E3, F_E4, F_VX, F_COUNT };
-template <int N, int LPQ>
+template <int N, int LPQ, int SEGS = 32 / LPQ>
 struct RicWave {
-    static constexpr int NG = 64 / LPQ, SL = RS * 16 / LPQ;   // groups per wave, slots per lane
+    static constexpr int NG = 64 / LPQ, SL = SEGS * kRicSeg;   // groups per wave, slots per lane
     // stage records of the groups; the polish verification scratch [SL][64] aliases them
     double recbuf[NG * N * REC > SL * 64 ? NG * N * REC : SL * 64];
     double w[SL][64];         // w = w0 - E x0 per (slot, lane)
@@ -297,7 +297,12 @@ struct MtH {
 // file and the LDS of a CU holds the same sixteen QPs in eight waves instead of four: the second wave fills
 // the issue slots the first leaves idle while it waits for its own dependent results.  The matrix-core passes
 // then carry two QPs in blocks 0 and 1; blocks 2 and 3 repeat them (same loads, same values stored).
-template <int N, int WPB, class SP, bool HET = false, int MODE = 0, int LPQ = 16>
+//
+// SEGS = slot segments per lane.  With 16 lanes per QP the default is two (the round-2 layout, 16 row slots per
+// lane); SEGS = 1 with 16 lanes is the layout for short horizons whose rows fit the first segment alone (N <= 16,
+// capi.hip::riccati_layout, DevProblem::rone): FOUR QPs per wavefront at the per-lane state of the 32-lane
+// layout, so eight waves of four QPs share a CU -- twice the QPs per instruction.
+template <int N, int WPB, class SP, bool HET = false, int MODE = 0, int LPQ = 16, int SEGS = 32 / LPQ>
 __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWork W, const double* __restrict__ x0_all,
                                                                const double* __restrict__ xref_all,
                                                                double* __restrict__ u_all, int64_t ld_u,
@@ -319,9 +324,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     __shared__ __attribute__((aligned(16))) RicShared<N> sh;
     constexpr int GL = LPQ;            // lanes of a group (one QP)
     constexpr int NG = 64 / LPQ;       // groups per wavefront
-    constexpr int NSG = 32 / LPQ;      // row-slot segments per lane
+    constexpr int NSG = SEGS;          // row-slot segments per lane
+    static_assert(LPQ * SEGS <= 32 && (SEGS == 1 || SEGS == 2), "a group's lanes hold at most the table's 32 segments");
     constexpr int SL = NSG * RSEG;     // row slots per lane
-    __shared__ __attribute__((aligned(16))) RicWave<N, LPQ> wscr[WPB];
+    __shared__ __attribute__((aligned(16))) RicWave<N, LPQ, SEGS> wscr[WPB];
     const int nseg = T.nseg;
     int home = 0;
     if (nseg > 1) {
@@ -385,7 +391,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // slot s of this lane in the problem's slot table (see kTab)
     const int j16 = lane & 15, sbase = LPQ == 32 ? ((lane >> 4) & 1) * RSEG : 0;
     auto tix = [&](int s) { return (sbase + s) * G16 + j16; };
-    RicWave<N, LPQ>& wv = wscr[wave];
+    RicWave<N, LPQ, SEGS>& wv = wscr[wave];
     double* rec = wv.recbuf + g * (N * REC);
     double(*scr)[64] = reinterpret_cast<double(*)[64]>(wv.recbuf);
     const bool boxed = P.boxed != 0;
@@ -1587,15 +1593,23 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
 constexpr int ric_lpq(int mode, bool het) {
     return het ? CARMPC_RIC_LPQ_HET : mode == 1 ? CARMPC_RIC_LPQ_M1 : mode == 2 ? CARMPC_RIC_LPQ_M2 : CARMPC_RIC_LPQ_M0;
 }
-// Wavefronts per workgroup: 16 QPs per workgroup where a CU's LDS (160 KB) holds them, fewer for longer horizons.
-template <int N, int LPQ>
+// Wavefronts per workgroup: eight with one slot segment per lane (two waves per SIMD at 256 registers), four with
+// two segments (one wave per SIMD), fewer where a CU's LDS (160 KB) does not hold that many.
+template <int N, int LPQ, int SEGS = 32 / LPQ>
 constexpr int ric_wpb_for() {
-    int w = 4 * LPQ / 16;
-    while (w > 1 && sizeof(RicShared<N>) + 16 + (size_t)w * sizeof(RicWave<N, LPQ>) > 160u * 1024u) --w;
+    int w = 8 / SEGS;
+    while (w > 1 && sizeof(RicShared<N>) + 16 + (size_t)w * sizeof(RicWave<N, LPQ, SEGS>) > 160u * 1024u) --w;
     return w;
 }
-// Horizons with a compiled instantiation (others run on the staged / dense kernels).
+// Horizons with a compiled instantiation (others run on the staged / dense kernels) ...
 #define RIC_FOR_EACH_N(X, ...) X(5, __VA_ARGS__) X(10, __VA_ARGS__) X(15, __VA_ARGS__) X(20, __VA_ARGS__) X(25, __VA_ARGS__)
+// ... and those that also have the four-QPs-per-wave form (16 lanes, one segment) for shared-model problems.
+#define RIC_FOR_EACH_N_ONESEG(X, ...) X(5, __VA_ARGS__) X(10, __VA_ARGS__)
+#ifdef CARMPC_NO_ONESEG   // A/B builds
+constexpr bool ric_has_oneseg(int) { return false; }
+#else
+constexpr bool ric_has_oneseg(int N) { return N == 5 || N == 10; }
+#endif
 
 // The kernel is compiled in several translation units (ipm_riccati_m0 / _m1 / _m2 / _het.hip: one per launch
 // kind, each with the code-generation flags that suit it, carmpc_amd/build.py) and launched from
@@ -1606,7 +1620,11 @@ constexpr int ric_wpb_for() {
     ipm_riccati_kernel<NN, ric_wpb_for<NN, ric_lpq(MODE, HET)>(), BicycleModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS); \
     PREFIX template __global__ void                                                                                   \
     ipm_riccati_kernel<NN, ric_wpb_for<NN, ric_lpq(MODE, HET)>(), DenseModel, HET, MODE, ric_lpq(MODE, HET)>(RIC_KERNEL_ARGS);
+#define RIC_INST_N1(NN, PREFIX, MODE)                                                                                  \
+    PREFIX template __global__ void ipm_riccati_kernel<NN, ric_wpb_for<NN, 16, 1>(), BicycleModel, false, MODE, 16, 1>(RIC_KERNEL_ARGS); \
+    PREFIX template __global__ void ipm_riccati_kernel<NN, ric_wpb_for<NN, 16, 1>(), DenseModel, false, MODE, 16, 1>(RIC_KERNEL_ARGS);
 #define RIC_INST(PREFIX, HET, MODE) RIC_FOR_EACH_N(RIC_INST_N, PREFIX, HET, MODE)
+#define RIC_INST_ONESEG(PREFIX, MODE) RIC_FOR_EACH_N_ONESEG(RIC_INST_N1, PREFIX, MODE)
 
 }  // namespace ric
 }  // namespace carmpc

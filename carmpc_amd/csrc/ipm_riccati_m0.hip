@@ -4,6 +4,7 @@
 namespace carmpc {
 namespace ric {
 RIC_INST(, false, 0)
+RIC_INST_ONESEG(, 0)
 }  // namespace ric
 }  // namespace carmpc
 RIC_TIMING_READER(m0)

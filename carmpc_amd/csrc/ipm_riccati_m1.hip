@@ -4,6 +4,7 @@
 namespace carmpc {
 namespace ric {
 RIC_INST(, false, 1)
+RIC_INST_ONESEG(, 1)
 }  // namespace ric
 }  // namespace carmpc
 RIC_TIMING_READER(m1)

@@ -4,6 +4,7 @@
 namespace carmpc {
 namespace ric {
 RIC_INST(, false, 2)
+RIC_INST_ONESEG(, 2)
 }  // namespace ric
 }  // namespace carmpc
 RIC_TIMING_READER(m2)

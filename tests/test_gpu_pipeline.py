@@ -68,3 +68,33 @@ def test_pipeline_with_disturbance_and_xref_equals_chunked_single_kernel(gpu_ava
     assert torch.equal(st1, st0) and torch.equal(it1, it0)
     assert int((st0 == 0).sum()) > B // 8
     assert torch.equal(u1, u0)
+
+
+def test_short_horizon_layouts_agree(gpu_available):
+    """N = 10 problems whose rows fit one slot segment run four QPs per wavefront from 16,384 instances on and
+    two per wavefront below: a batch solved whole (pipeline, four per wave), in chunks of 20,000 (single kernel,
+    four per wave) and in chunks of 4,000 (single kernel, two per wave) gives the same statuses and iteration
+    counts, and u to 1e-12 (the layouts order their sums differently)."""
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build("RoadMultipleCarsEnv", 10, terminal_set_dir=TERMINAL_SETS)
+    qp = QPProblem(N=10, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    B = 60000
+    x = _x0(np.random.default_rng(17), asm.goal[0], B)
+    x[:, 0] = asm.goal[0] - (asm.goal[0] - x[:, 0]) * 0.5
+    X = torch.as_tensor(x).to(qp.device)
+    u0, s0, i0 = qp.solve(X)
+    torch.cuda.synchronize()
+    assert int((s0 == 0).sum()) > B // 8
+    for chunk in (20000, 4000):
+        parts = [qp.solve(X[i:i + chunk]) for i in range(0, B, chunk)]
+        torch.cuda.synchronize()
+        u1 = torch.cat([p[0] for p in parts]); s1 = torch.cat([p[1] for p in parts]); i1 = torch.cat([p[2] for p in parts])
+        assert torch.equal(s1, s0), chunk
+        same = float((i1 == i0).double().mean())
+        assert same >= 0.999 and int((i1 - i0).abs().max()) <= 2, (chunk, same)
+        ok = (s0 == 0)
+        assert float((u1[ok] - u0[ok]).abs().max()) <= 1e-9, chunk

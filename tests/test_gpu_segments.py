@@ -143,7 +143,9 @@ def test_pipeline_runs_that_do_not_start_at_instance_zero(gpu_available, case):
         sl = slice(int(offsets[j]), int(offsets[j + 1]))
         u1, s1, i1 = p.solve(X[sl])
         torch.cuda.synchronize()
-        assert torch.equal(s1, st[sl]) and torch.equal(i1, it[sl])
+        bad = ((s1 != st[sl]) | (i1 != it[sl])).nonzero().flatten()
+        assert bad.numel() == 0, (case, j, bad[:8].tolist(), s1[bad[:8]].tolist(), st[sl][bad[:8]].tolist(),
+                                  i1[bad[:8]].tolist(), it[sl][bad[:8]].tolist(), int(bad.numel()))
         ok = s1 == 0
         assert int(ok.sum()) > 0
         assert float((u1[ok] - u[sl, :p.n][ok]).abs().max()) <= 1e-12
