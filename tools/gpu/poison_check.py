@@ -1,0 +1,85 @@
+"""Pipeline against single-kernel solves with the LDS of every CU and the stream-ordered memory pool filled with a
+chosen bit pattern before each call (build/probe/libpoison.so, tools/probe/lds_poison.hip): a read of LDS or work-list
+memory ahead of its write then meets the pattern instead of the previous launch's leftovers.
+Usage: python tools/gpu/poison_check.py [trials]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
+from conftest import TERMINAL_SETS  # noqa: E402
+from carmpc_amd.configuration import DT_CONTROL, LINEARIZE_INPUT, LINEARIZE_STATE  # noqa: E402
+from carmpc_amd.environments import ENVIRONMENTS  # noqa: E402
+from carmpc_amd.mpc import MPCStateFB  # noqa: E402
+from carmpc_amd.qp import solve_segments  # noqa: E402
+
+lib = ctypes.CDLL(os.path.join(os.path.dirname(__file__), "..", "..", "build", "probe", "libpoison.so"))
+lib.poison_lds.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+lib.poison_pool.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p]
+
+PATTERNS = {"nan": 0x7FF8000000000000, "ones": 0xFFFFFFFFFFFFFFFF, "zero": 0, "huge": 0x7FE0000000000000,
+            "neg1": 0xBFF0000000000000, "small_int": 0x0000000300000003, "none": None}
+
+
+def poison(name):
+    pat = PATTERNS[name]
+    if pat is None:
+        return
+    assert lib.poison_lds(pat, 4096, None) == 0
+    assert lib.poison_pool(pat, 64 << 20, None) == 0
+
+
+def states(n, seed):
+    rng = np.random.default_rng(seed)
+    return np.column_stack([rng.uniform(0, 28, n), rng.uniform(-2.5, 2.5, n), rng.uniform(-0.3, 0.3, n), rng.uniform(0, 4, n)])
+
+
+def main():
+    trials = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    p20 = [MPCStateFB(dt=DT_CONTROL, N=20, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT, env=ENVIRONMENTS[e](),
+                      terminal_set_dir=TERMINAL_SETS).qp for e in ("RoadEnv", "RoadOneCarEnv", "RoadMultipleCarsEnv")]
+    p10 = MPCStateFB(dt=DT_CONTROL, N=10, lin_state=LINEARIZE_STATE, lin_input=LINEARIZE_INPUT, env=ENVIRONMENTS["RoadEnv"](),
+                     terminal_set_dir=TERMINAL_SETS).qp
+    cases = {"first_offset_positive": ([p20[1], p20[2]], np.array([5000, 33000, 61000])),
+             "leading_other_horizon": ([p10, p20[0], p20[2]], np.array([0, 3000, 30000, 56000]))}
+    total_bad = 0
+    for name, (probs, offsets) in cases.items():
+        B = int(offsets[-1]) + 100
+        X = torch.as_tensor(states(B, 21)).cuda()
+        # reference: per-problem solves without poison
+        ref = []
+        for j, p in enumerate(probs):
+            sl = slice(int(offsets[j]), int(offsets[j + 1]))
+            ref.append(tuple(t.clone() for t in p.solve(X[sl])))
+        torch.cuda.synchronize()
+        for pat in PATTERNS:
+            for trial in range(trials):
+                for which in ("segments", "single"):
+                    poison(pat)
+                    if which == "segments":
+                        u = torch.full((B, 40), -7.0, dtype=torch.float64, device="cuda")
+                        st = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+                        it = torch.full((B,), -7, dtype=torch.int32, device="cuda")
+                        solve_segments(probs, offsets, X, out=(u, st, it))
+                        got = [(u[int(offsets[j]):int(offsets[j + 1]), :p.n], st[int(offsets[j]):int(offsets[j + 1])],
+                                it[int(offsets[j]):int(offsets[j + 1])]) for j, p in enumerate(probs)]
+                    else:
+                        got = [p.solve(X[int(offsets[j]):int(offsets[j + 1])]) for j, p in enumerate(probs)]
+                    torch.cuda.synchronize()
+                    for j, ((u1, s1, i1), (u0, s0, i0)) in enumerate(zip(got, ref)):
+                        bad = ((s1 != s0) | (i1 != i0)).nonzero().flatten()
+                        if bad.numel():
+                            total_bad += int(bad.numel())
+                            b8 = bad[:8]
+                            print("MISMATCH", name, pat, trial, which, "seg", j, "count", int(bad.numel()), "idx", b8.tolist(),
+                                  "status", s1[b8].tolist(), "ref", s0[b8].tolist(), "iters", i1[b8].tolist(), "ref", i0[b8].tolist(),
+                                  flush=True)
+                print("done", name, pat, trial, flush=True)
+    print("total mismatches", total_bad)
+
+
+if __name__ == "__main__":
+    main()
