@@ -301,6 +301,10 @@ struct RicWork {
     uint32_t* pend_rec;   // total x kRicRecWords: hand-off records in hand-off order
     int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
     int32_t round;        // pipeline round of this launch
+    // The last tail[j] instances of segment j skip the iteration and polish launches: the final launch (single kernel)
+    // takes them as fresh instances behind the retry list, so that it has work for the group slots that its few, long
+    // retries leave idle.
+    int32_t tail[kRicMaxSeg];
 };
 // One round of (iterations, polish): a second one for the instances whose polish was rejected measured
 // slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 2-3 % with the

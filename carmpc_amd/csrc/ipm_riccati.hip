@@ -24,6 +24,10 @@ bool riccati_supported_N(int N) {
 
 bool riccati_oneseg_N(int N) { return ric_has_oneseg(N); }
 constexpr int64_t kRicOneSegMin = 16384;
+#ifndef CARMPC_RIC_TAIL_DIV
+#define CARMPC_RIC_TAIL_DIV 32
+#endif
+constexpr int kRicTailDiv = CARMPC_RIC_TAIL_DIV;
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
@@ -100,6 +104,16 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
     W.pend_rec = reinterpret_cast<uint32_t*>(W.cnt + ncnt);   // (ncnt words = 256 bytes: records stay line-aligned)
     W.retry_idx = reinterpret_cast<int32_t*>(W.pend_rec + (size_t)kRicRecWords * n);
     e = launch_zero_u32(W.cnt, (int)ncnt, stream);
+    // the final launch's fresh instances (RicWork::tail): 1/kRicTailDiv of every segment
+#ifdef CARMPC_RIC_TAIL_ENV   // experiment builds only: divisor from the environment
+    static const int tail_div = [] {
+        const char* v = getenv("CARMPC_RIC_TAIL_DIV");
+        return v ? atoi(v) : kRicTailDiv;
+    }();
+#else
+    constexpr int tail_div = kRicTailDiv;
+#endif
+    for (int j = 0; j < T.nseg; ++j) W.tail[j] = tail_div > 0 ? (int32_t)((T.off[j + 1] - T.off[j]) / tail_div) : 0;
     // rounds of (iterations, polish): round r takes the instances whose first r polishes were rejected
     // (two or three per cent after round 0); what is left after the last round goes to the single kernel
     for (W.round = 0; W.round < kRicRounds && e == hipSuccess; ++W.round) {

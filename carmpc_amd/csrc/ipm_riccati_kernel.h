@@ -1079,12 +1079,20 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
         return (int64_t)__shfl(v, lane & ~(GL - 1), 64);
     };
     // closed-loop runs solve only their live instances: slot -> row through S.index, count on device
-    const int64_t nlive = S.count ? (int64_t)*S.count : batch;
+    // launch pipeline: the iteration launch leaves the segment's last W.tail instances to the final launch, which takes
+    // them as fresh instances behind its retry list (slots nretry .. nretry + tail - 1)
+    const int64_t ntail = W.cnt ? (int64_t)W.tail[seg] : 0;
+    const int64_t nretry = (MODE == 0 && W.cnt) ? (int64_t)*S.count : 0;
+    const int64_t nlive = (MODE == 0 && W.cnt) ? nretry + ntail
+                          : S.count            ? (int64_t)*S.count
+                          : (MODE == 1 && W.cnt) ? batch - ntail
+                                                 : batch;
     int64_t slot = S.claim ? claim() : ((int64_t)blockIdx.x * WPB + wave) * NG + g;
     bool live = slot < nlive;   // the group has an instance to work on
     // slot -> row: the caller's list, the hand-off record (polish launch), or the slot itself
     auto row_of = [&](int64_t sl, bool lv) -> int64_t {
         if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(lst0 + sl) * kRicRecWords + kRicRecRow] : sl;
+        else if (MODE == 0 && W.cnt) return !lv ? sl : sl < nretry ? (int64_t)S.index[sl] : batch - ntail + (sl - nretry);
         else return lv && S.index ? (int64_t)S.index[sl] : sl;
     };
     int64_t inst = row_of(slot, live);
@@ -1465,7 +1473,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         // instance's first r polishes are known to be rejected -- that is why it is here;
                         // pass them over the way the single kernel carries on after a rejection: same
                         // iterate, no polish until a step has been taken
-                        if (W.cnt && polish && npol < W.round) {
+                        if (W.cnt && polish && npol < W.round && slot < nretry) {
                             ++npol;
                             polish = false;
                         }
