@@ -431,11 +431,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // owner (lane N - 1) and every overflow lane sit in the group's upper DPP row, the lower row contributes
     // zeros: the 16-lane butterfly is the whole sum there (the lower row's lanes get a value nobody reads).
     constexpr bool kStageNUpperRow = LPQ == 32 && N >= 17;
-    auto stageN_sum = [&](double v) __attribute__((always_inline)) {
-        if constexpr (kStageNUpperRow) return lanes::row_reduce<OpSum>(v);
-        else return grp_reduce<LPQ, OpSum>(v);
-    };
-    // ... two of them at a time (lanes.h: the second value rides in the lower row through the same butterfly)
+    // Two totals at a time (lanes.h: the second value rides in the lower row through the same butterfly).
     auto stageN_sum2 = [&](double& a, double& b) __attribute__((always_inline)) {
         if constexpr (kStageNUpperRow) upper_row_sum2(a, b);
         else grp_reduce2<LPQ, OpSum>(a, b);
