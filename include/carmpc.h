@@ -93,7 +93,8 @@ typedef struct {
                           workgroup, 4-6 = staged variants of experiment builds only (rejected
                           with CARMPC_EUNSUPPORTED otherwise), 7 = grouped stage-form
                           (Riccati) kernel, 32 lanes per QP (assembled, nu=2, N in
-                          {5,10,15,20,25}, <= 8 rows per stage) */
+                          {5,10,15,20,25}, <= 8 rows per stage; N = 5, 10 with all rows in
+                          the first 16 lanes' slots: 16 lanes per QP from 16,384 instances on) */
 } carmpc_settings;
 
 /* Which solve kernel `auto` picks for this problem: 1 dense, 2 staged, 7 grouped Riccati. */
