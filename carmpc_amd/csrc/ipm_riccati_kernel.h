@@ -89,6 +89,9 @@ static __device__ unsigned long long carmpc_ric_cycles[12];
 #define RIC_WRITER true
 #endif
 // Stages of read-ahead of the matrix-core passes (see the comment at kPre).
+#ifndef CARMPC_RIC_FACTOR_SPLIT   // 1: with two QPs per wave, blocks 2 and 3 take the vector half of the factorization
+#define CARMPC_RIC_FACTOR_SPLIT 1
+#endif
 #ifndef CARMPC_RIC_KPRE
 #define CARMPC_RIC_KPRE 1
 #endif
@@ -985,6 +988,77 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 const int r = (t + 1) * REC;
                 recm[r + oK] = mm(o[t + 1].En, o[t + 1].Z, 0.0);       // rows 0-1: E'D E F = Re^{-1} F
                 recm[r + oKPt] = mm(o[t + 1].En, o[t + 1].zg, 0.0);    // rows 0-1: Re^{-1} g
+                recm[r + O_CH] = o[t + 1].l;
+                recm[r + oDrow] = o[t + 1].drow;
+            }
+            stage_fence();
+        }
+        wb();
+    };
+    // The same with two QPs per wave.  Blocks 2 and 3 would repeat blocks 0 and 1 (same loads, same products); instead
+    // they carry the VECTOR half of every stage -- b^x + A'p, E (b^u + B'p), the p recursion, kappa -- in the very
+    // instructions whose matrix half (Qbar + W + A'PA, E B'PA, the P recursion, K) blocks 0 and 1 compute: the two
+    // halves share the left operand (A, [B 0 0] E', Y, E) and differ in the right operand and the addend, which are one
+    // register each with the matrix value in lanes 0..7 of a DPP row and the vector value in lanes 8..15.  What the
+    // vector half needs from the matrix half -- l, the pivots' reciprocals, Y -- crosses once per stage (row_shr:8).
+    // Ten products per stage instead of fourteen, three record loads instead of six; every product is the one the
+    // unsplit pass computes, bit for bit.
+    constexpr bool kFactorSplit = NG == 2 && CARMPC_RIC_FACTOR_SPLIT != 0;
+    auto factor_mm_split = [&]() __attribute__((always_inline)) {
+        wb();
+        const PassK pk = pass_consts();
+        const double cB0m1 = pk.cB0m1, k10 = pk.k10, kd = pk.kd;
+        int lz = lane;
+        asm volatile("" : "+v"(lz));
+        const bool vrole = ((lz >> 3) & 1) != 0;   // blocks 2, 3
+        const double cAm = vrole ? 0.0 : cA, cQm = vrole ? 0.0 : cQ;
+        // the three record fields per stage: (Db_0, Db_1, W_t) for the matrix half, (b^u in rows 0-1, b^u_0 in row 1,
+        // b^x_t) for the vector half; W_t and b^x_t sit in the record of stage t - 1
+        const int o1 = vrole ? oBUt : O_DB, o2 = vrole ? oBU1 : O_DB + 1, o3 = vrole ? O_BX + (lz >> 4) : oW;
+        const int oKK = vrole ? oKPt : oK;
+        struct In { double l1, l2, l3; };
+        struct Out { double En, ZZ, l, drow; };
+        In in[N];
+        Out o[N];
+        auto load = [&](int t) {
+            const int r = t * REC, rp = (t >= 1 ? t - 1 : 0) * REC;
+            in[t].l1 = recm[r + o1];
+            in[t].l2 = recm[r + o2];
+            in[t].l3 = recm[rp + o3];
+        };
+        double PP = (vrole ? 0.0 : cPt) + recm[(N - 1) * REC + o3];   // P + W_N | b^x_N
+#pragma unroll
+        for (int t = N - 1; t >= 0 && t > N - 1 - kPre; --t) load(t);
+        stage_fence();
+#pragma unroll
+        for (int t = N - 1; t >= -1; --t) {
+            if (t - kPre >= 0) load(t - kPre);
+            if (t >= 0) {
+                const double X = mm(PP, cAm, vrole ? PP : 0.0);   // P A | p
+                const double PB0 = mm(PP, cB0r, 0.0);             // (matrix half; the vector half's results are not used)
+                const double PB1 = mm(PP, cB1r, 0.0);
+                const double re00 = mm(cB0r, PB0, MT.R[0] + in[t].l1);
+                const double re10 = mm(cB1r, PB0, MT.R[2]);
+                const double re11 = mm(cB1r, PB1, MT.R[3] + in[t].l2);
+                const double AP = mm(cA, X, cQm + in[t].l3);      // Qbar_t + W_t + A'(P A) | b^x_t + A'p
+                const double p0 = re00 > 0.0 ? re00 : 1e128;
+                const double det = fma(p0, re11, -(re10 * re10));
+                const double r0 = frcp(p0);
+                const double rd = frcp(det > 0.0 ? det : 1.0);
+                const double ip1 = det > 0.0 ? p0 * rd : 1e-128;
+                const double l = upper_half_from_lower(re10 * r0);
+                const double drow = upper_half_from_lower(mr == 0 ? r0 : ip1);
+                const double Xl = fma(-l, cB0m1, cBp);            // [B 0 0] E'
+                const double YY = mm(Xl, X, vrole ? fma(-l, in[t].l2, in[t].l1) : 0.0);   // E B'PA | E (b^u + B'p)
+                o[t].En = fma(-l, k10, kd);
+                o[t].ZZ = YY * drow;
+                o[t].l = l;
+                o[t].drow = drow;
+                PP = mm_na(upper_half_from_lower(YY), o[t].ZZ, AP);   // P_t | p_t
+            }
+            if (t + 1 < N) {
+                const int r = (t + 1) * REC;
+                recm[r + oKK] = mm(o[t + 1].En, o[t + 1].ZZ, 0.0);     // Re^{-1} F | Re^{-1} g   (rows 0-1)
                 recm[r + O_CH] = o[t + 1].l;
                 recm[r + oDrow] = o[t + 1].drow;
             }

@@ -61,6 +61,16 @@ __device__ __forceinline__ void swap16(double& x, double& y) {   // rows of x: (
     x = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
     y = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
 }
+// Lanes 8..15 of every DPP row take the value of the lane 8 below them, lanes 0..7 keep theirs (row_shr:8 into
+// banks 2 and 3).  In the matrix-core layout (block b = lanes 4 b .. 4 b + 3 of each row) that copies blocks 0, 1
+// onto blocks 2, 3.
+__device__ __forceinline__ double upper_half_from_lower(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)b, (int)(unsigned)b, 0x118, 0xf, 0xc, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(b >> 32), (int)(unsigned)(b >> 32), 0x118, 0xf, 0xc, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
 template <int LPQ, class Op>
 __device__ __forceinline__ void grp_reduce2(double& a, double& b) {
     if constexpr (LPQ == 32) {
