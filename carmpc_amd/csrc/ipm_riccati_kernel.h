@@ -184,8 +184,8 @@ struct RicShared {
     int32_t partner[kTab];
     double lb[64], ub[64];
 };
-// per-input state of the owned inputs, one row of 12 fields x 2 components per input pair t
-// (row N: dummy row written by lanes whose segment owns no input)
+// per-input state of the owned inputs: 12 fields x 2 components per input pair t (row t; row N: dummy row
+// written by lanes whose segment owns no input)
 enum { F_U = 0, F_Q, F_SU, F_SL, F_ZU, F_ZL, F_RD, F_E1, F_E2, F_E3, F_E4, F_VX, F_COUNT };
 template <int N, int LPQ, int SEGS = 32 / LPQ>
 struct RicWave {
@@ -193,7 +193,10 @@ struct RicWave {
     // stage records of the groups; the polish verification scratch [SL][64] aliases them
     double recbuf[NG * N * REC > SL * 64 ? NG * N * REC : SL * 64];
     double w[SL][64];         // w = w0 - E x0 per (slot, lane)
-    double vbox[NG][N + 1][F_COUNT * 2];
+    // Field-major: the N + 1 rows of one field are contiguous (16 bytes per row), so the lanes of a group -- lane l on
+    // row l -- read and write consecutive 16-byte slots, one per bank group.  (Row-major rows of 192 bytes put lanes
+    // l, l + 4, l + 8, ... on the same banks: five-way conflicts on every access.)
+    double vbox[NG][F_COUNT][N + 1][2];
 };
 
 __device__ __forceinline__ void wb() { __builtin_amdgcn_wave_barrier(); }
@@ -410,8 +413,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     }
     double* vb[NSG];
 #pragma unroll
-    for (int sg = 0; sg < NSG; ++sg) vb[sg] = &wv.vbox[g][own[sg] ? kseg[sg] - 1 : N][0];
-#define BX(F, sg, c) vb[sg][(F) * 2 + (c)]
+    for (int sg = 0; sg < NSG; ++sg) vb[sg] = &wv.vbox[g][0][own[sg] ? kseg[sg] - 1 : N][0];
+#define BX(F, sg, c) vb[sg][(F) * ((N + 1) * 2) + (c)]
     // Unused row slots are made inert instead of being masked: their coefficients are zero, w = 1,
     // s = 1, z = 0, so every residual, direction and sum below gets an exact zero from them and the
     // slot loops are straight-line code (no exec-mask region per slot).  The validity bits are only
