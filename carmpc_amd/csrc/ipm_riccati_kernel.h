@@ -116,7 +116,9 @@ using namespace lanes;
 constexpr int G16 = kRicLanes;
 constexpr int RSEG = kRicSeg;
 constexpr int RS = kRicSlots;
-constexpr int REC = 20;   // doubles per stage record (160 B)
+// Doubles per stage record: 20 fields; two more of padding where the LDS has room for them (ric_rec below), which
+// spreads the records of consecutive stages -- one per lane in the row phases -- over all banks.
+constexpr int kRecFields = 20;
 // record t (stage t+1, input t):
 //   [0..9]   W_{t+1} (packed) | lamZ_{t+1} [0..3], lamH_{t+1} [4..7] | factor: K_t [0..7], il00 l10 il11 [8..10]
 //   [12..15] b^x_{t+1} | y_{t+1} | gz_t [12..13], hs_t [14..15]
@@ -181,23 +183,57 @@ template <int N>
 struct RicShared {
     double2 cf01[kTab];   // c~0, c~1
     double2 cf23[kTab];   // c~2, c~3
-    int32_t partner[kTab];
-    double lb[64], ub[64];
+    int16_t partner[kTab];
+    double lb[2 * N], ub[2 * N];
 };
 // per-input state of the owned inputs: 12 fields x 2 components per input pair t (row t; row N: dummy row
 // written by lanes whose segment owns no input)
 enum { F_U = 0, F_Q, F_SU, F_SL, F_ZU, F_ZL, F_RD, F_E1, F_E2, F_E3, F_E4, F_VX, F_COUNT };
-template <int N, int LPQ, int SEGS = 32 / LPQ>
-struct RicWave {
+// REC_ doubles per stage record, QS_ doubles between the records of two groups (see ric_rec, ric_qstride)
+template <int N, int LPQ, int SEGS, int REC_, int QS_>
+struct RicWaveT {
     static constexpr int NG = 64 / LPQ, SL = SEGS * kRicSeg;   // groups per wave, slots per lane
     // stage records of the groups; the polish verification scratch [SL][64] aliases them
-    double recbuf[NG * N * REC > SL * 64 ? NG * N * REC : SL * 64];
+    double recbuf[NG * QS_ > SL * 64 ? NG * QS_ : SL * 64];
     double w[SL][64];         // w = w0 - E x0 per (slot, lane)
     // Field-major: the N + 1 rows of one field are contiguous (16 bytes per row), so the lanes of a group -- lane l on
     // row l -- read and write consecutive 16-byte slots, one per bank group.  (Row-major rows of 192 bytes put lanes
     // l, l + 4, l + 8, ... on the same banks: five-way conflicts on every access.)
     double vbox[NG][F_COUNT][N + 1][2];
 };
+// LDS banking of the stage records (64 banks of 4 bytes for 8- and 16-byte reads, 32 for stores; a 16-byte access is
+// served in groups of 8 or 16 lanes).  In the row phases lane l works on record l: at 20 doubles per record lanes
+// l, l + 8, l + 16 share banks; 22 doubles put the 16-byte slots of 16 consecutive records on 16 different bank
+// groups.  In the matrix-core passes the blocks of two QPs access the same fields of their records at once: the
+// distance between the two QPs' records decides whether those meet on a bank.  Two QPs per wave: the distance in
+// dwords is kept at 16..24 or 40..48 modulo 64 (reads: 14 banks per QP) and away from 0 modulo 32 (stores).
+constexpr int ric_qstride(int N, int rec, int ng) {
+    if (ng != 2) return N * rec;
+    for (int pad = 0; pad < 32; pad += 2) {
+        const int d = 2 * (N * rec + pad);
+        if ((d % 64 >= 16 && d % 64 <= 24) || (d % 64 >= 40 && d % 64 <= 48)) return N * rec + pad;
+    }
+    return N * rec;
+}
+constexpr int ric_waves_wanted(int SEGS) { return 8 / SEGS; }
+template <int N, int LPQ, int SEGS, int REC_>
+constexpr size_t ric_lds_bytes(int waves) {
+    return sizeof(RicShared<N>) + 16 + (size_t)waves * sizeof(RicWaveT<N, LPQ, SEGS, REC_, ric_qstride(N, REC_, 64 / LPQ)>);
+}
+// waves per workgroup: as many as a CU's LDS (160 KB) holds, up to eight with one slot segment per lane and four with two
+template <int N, int LPQ, int SEGS, int REC_>
+constexpr int ric_wpb_rec() {
+    int w = ric_waves_wanted(SEGS);
+    while (w > 1 && ric_lds_bytes<N, LPQ, SEGS, REC_>(w) > 160u * 1024u) --w;
+    return w;
+}
+// the padded record where it costs no wave
+template <int N, int LPQ, int SEGS>
+constexpr int ric_rec() {
+    return (64 / LPQ == 2 && ric_wpb_rec<N, LPQ, SEGS, kRecFields + 2>() == ric_wpb_rec<N, LPQ, SEGS, kRecFields>()) ? kRecFields + 2 : kRecFields;
+}
+template <int N, int LPQ, int SEGS = 32 / LPQ>
+using RicWave = RicWaveT<N, LPQ, SEGS, ric_rec<N, LPQ, SEGS>(), ric_qstride(N, ric_rec<N, LPQ, SEGS>(), 64 / LPQ)>;
 
 __device__ __forceinline__ void wb() { __builtin_amdgcn_wave_barrier(); }
 
@@ -333,6 +369,8 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     constexpr int NSG = SEGS;          // row-slot segments per lane
     static_assert(LPQ * SEGS <= 32 && (SEGS == 1 || SEGS == 2), "a group's lanes hold at most the table's 32 segments");
     constexpr int SL = NSG * RSEG;     // row slots per lane
+    constexpr int REC = ric_rec<N, LPQ, SEGS>();               // doubles per stage record
+    constexpr int QS = ric_qstride(N, REC, NG);                // doubles between the records of two groups
     __shared__ __attribute__((aligned(16))) RicWave<N, LPQ, SEGS> wscr[WPB];
     const int nseg = T.nseg;
     int home = 0;
@@ -382,10 +420,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     for (int i = threadIdx.x; i < kTab; i += blockDim.x) {
         sh.cf01[i] = make_double2(P.r_coef[i * 4 + 0], P.r_coef[i * 4 + 1]);
         sh.cf23[i] = make_double2(P.r_coef[i * 4 + 2], P.r_coef[i * 4 + 3]);
-        sh.partner[i] = P.r_partner ? P.r_partner[i] : -1;
+        sh.partner[i] = (int16_t)(P.r_partner ? P.r_partner[i] : -1);
     }
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) {
-        const bool bx = i < 2 * N && P.boxed;
+    for (int i = threadIdx.x; i < 2 * N; i += blockDim.x) {
+        const bool bx = P.boxed;
         sh.lb[i] = bx ? P.lb[i] : -UNBOXED_BOUND;
         sh.ub[i] = bx ? P.ub[i] : UNBOXED_BOUND;
     }
@@ -398,7 +436,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     const int j16 = lane & 15, sbase = LPQ == 32 ? ((lane >> 4) & 1) * RSEG : 0;
     auto tix = [&](int s) { return (sbase + s) * G16 + j16; };
     RicWave<N, LPQ, SEGS>& wv = wscr[wave];
-    double* rec = wv.recbuf + g * (N * REC);
+    double* rec = wv.recbuf + g * QS;
     double(*scr)[64] = reinterpret_cast<double(*)[64]>(wv.recbuf);
     const bool boxed = P.boxed != 0;
     // segment stages: seg 0 -> j+1, seg 1 -> j+17 (overflow segments -> stage N)
@@ -859,7 +897,7 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     //     which always holds 0.0, and lanes whose result is a structural zero store it there;
     //   * lanes that hold copies of one value (the columns of a vector) all store it.
     const int mb = (lane >> 2) & 3, mr = lane >> 4, mc = lane & 3;
-    double* recm = wv.recbuf + (mb % NG) * (N * REC);
+    double* recm = wv.recbuf + (mb % NG) * QS;
     auto mm = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0); };
     auto mm_na = [](double a, double b, double c) { return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 1); };
     const bool m_top = mr < 2, m_left = mc < 2;
@@ -1678,9 +1716,7 @@ constexpr int ric_lpq(int mode, bool het) {
 // two segments (one wave per SIMD), fewer where a CU's LDS (160 KB) does not hold that many.
 template <int N, int LPQ, int SEGS = 32 / LPQ>
 constexpr int ric_wpb_for() {
-    int w = 8 / SEGS;
-    while (w > 1 && sizeof(RicShared<N>) + 16 + (size_t)w * sizeof(RicWave<N, LPQ, SEGS>) > 160u * 1024u) --w;
-    return w;
+    return ric_wpb_rec<N, LPQ, SEGS, ric_rec<N, LPQ, SEGS>()>();
 }
 // Horizons with a compiled instantiation (others run on the staged / dense kernels) ...
 #define RIC_FOR_EACH_N(X, ...) X(5, __VA_ARGS__) X(10, __VA_ARGS__) X(15, __VA_ARGS__) X(20, __VA_ARGS__) X(25, __VA_ARGS__)
