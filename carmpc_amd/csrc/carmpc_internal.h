@@ -299,13 +299,22 @@ constexpr int kRicRecWords = 32, kRicRecX0 = 16, kRicRecRow = 24, kRicRecIt = 25
 struct RicWork {
     unsigned* cnt;
     uint32_t* pend_rec;   // total x kRicRecWords: hand-off records in hand-off order
-    int32_t* retry_idx;   // total: segment-relative rows whose polish was rejected
+    int32_t* retry_idx;   // total: hand-off records (positions in the segment's list) whose polish was rejected
     int32_t round;        // pipeline round of this launch
     // The last tail[j] instances of segment j skip the iteration and polish launches: the final launch (single kernel)
     // takes them as fresh instances behind the retry list, so that it has work for the group slots that its few, long
     // retries leave idle.
     int32_t tail[kRicMaxSeg];
+    // The iterate of every handed-off instance (slacks, multipliers, inputs, stage states: kRicStateDoubles per
+    // instance, indexed like pend_rec) for the first state_cap hand-offs of the run: a retry whose state is here resumes
+    // from it instead of repeating the iterations that led to the hand-off.  Null / 0: every retry starts over.
+    double* state;
+    int64_t state_cap;
 };
+// (2 x 8 row slots + 4 state entries + 5 box quantities x 2 inputs per lane, 32 lanes per QP; the 16-lane layouts need
+// as much or half of it)
+constexpr int kRicStateDoubles = 960;
+constexpr size_t kRicStateMaxBytes = (size_t)2 << 30;   // per call; hand-offs beyond it are not saved
 // One round of (iterations, polish): a second one for the instances whose polish was rejected measured
 // slower on the 131,072-instance mixed shard (10.9M vs 11.45M QP/s when 6 % were rejected; 2-3 % with the
 // correction round and the early polish gate) -- it solves them with the lean kernels but still leaves a

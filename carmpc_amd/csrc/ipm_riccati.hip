@@ -1,5 +1,6 @@
 // ipm_riccati.hip -- launch side of the grouped stage-form IPM kernel (ipm_riccati_kernel.h): grid sizing,
 // dispatch by horizon and model structure, the three-launch pipeline, several problems per launch.
+#include <mutex>
 #include "ipm_riccati_kernel.h"
 
 namespace carmpc {
@@ -28,6 +29,10 @@ constexpr int64_t kRicOneSegMin = 16384;
 #define CARMPC_RIC_TAIL_DIV 32
 #endif
 constexpr int kRicTailDiv = CARMPC_RIC_TAIL_DIV;
+#ifndef CARMPC_RIC_SAVE_STATE   // 0: A/B builds without the saved iterates (every retry starts over)
+#define CARMPC_RIC_SAVE_STATE 1
+#endif
+constexpr bool kRicSaveState = CARMPC_RIC_SAVE_STATE != 0;
 
 namespace {
 // grid = one workgroup per CU slot (persistent workgroups), at most one per 16 instances
@@ -91,20 +96,67 @@ hipError_t ric_dispatch(const RicSegs& T, const RicWork& W, int64_t total, const
 // The launch pipeline: rounds of iterations with hand-off and lock-step polish, then the single kernel for
 // what the last round rejected (see MODE at the kernel).  Work lists and counters live for the call,
 // stream-ordered.  The last launch usually finds an empty list; its workgroups read the count and return.
+// The pipeline's work memory (lists, counters, saved iterates: up to kRicStateMaxBytes + 132 B per instance, per call
+// in flight) is stream-ordered memory from a pool of the library's own per device, which keeps what a call frees for
+// the next one (release threshold: none) -- a caller that synchronises after every call would otherwise pay a device
+// allocation of that size per call.  Without such a pool (creation refused) the device's default pool serves.
+hipMemPool_t pipeline_pool() {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    static bool tried[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!tried[dev]) {
+        tried[dev] = true;
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t p = nullptr;
+        if (hipMemPoolCreate(&p, &props) == hipSuccess) {
+            uint64_t keep = UINT64_MAX;
+            if (hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess) pools[dev] = p;
+            else (void)hipMemPoolDestroy(p);
+        }
+        (void)hipGetLastError();   // (a refused pool is not an error of the call)
+    }
+    return pools[dev];
+}
+hipError_t pipeline_alloc(void** ptr, size_t bytes, hipStream_t stream) {
+    if (hipMemPool_t pool = pipeline_pool()) return hipMallocFromPoolAsync(ptr, bytes, pool, stream);
+    return hipMallocAsync(ptr, bytes, stream);
+}
+
 hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const double* xref, double* u_out, int64_t ld_u,
                         int32_t* status, int32_t* iters, const Settings& s, hipStream_t stream, int* unsupported) {
+    static_assert(kRicRounds == 1, "the retry list names hand-off records: a second round of iterations would need their rows");
     const size_t n = (size_t)total, ncnt = (size_t)kRicClaimStride * kRicMaxSeg;
     const size_t bytes = sizeof(unsigned) * ncnt + sizeof(uint32_t) * kRicRecWords * n + sizeof(int32_t) * n;
     static_assert(kRicLanes == kRicRecX0 && (kRicClaimStride * kRicMaxSeg * sizeof(unsigned)) % 128 == 0, "record layout");
     char* base = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&base), bytes, stream);
+    hipError_t e = pipeline_alloc(reinterpret_cast<void**>(&base), bytes, stream);
     if (e != hipSuccess) return e;
     RicWork W{};
     W.cnt = reinterpret_cast<unsigned*>(base);
     W.pend_rec = reinterpret_cast<uint32_t*>(W.cnt + ncnt);   // (ncnt words = 256 bytes: records stay line-aligned)
     W.retry_idx = reinterpret_cast<int32_t*>(W.pend_rec + (size_t)kRicRecWords * n);
+    // saved iterates of the hand-offs (RicWork::state); without the memory every retry starts over, as beyond the cap
+    const size_t state_one = sizeof(double) * kRicStateDoubles;
+    W.state_cap = kRicSaveState ? (int64_t)std::min(n, kRicStateMaxBytes / state_one) : 0;
+    void* state = nullptr;
+    if (W.state_cap > 0 && pipeline_alloc(&state, state_one * (size_t)W.state_cap, stream) != hipSuccess) {
+        (void)hipGetLastError();
+        state = nullptr;
+        W.state_cap = 0;
+    }
+    W.state = static_cast<double*>(state);
     e = launch_zero_u32(W.cnt, (int)ncnt, stream);
-    // the final launch's fresh instances (RicWork::tail): 1/kRicTailDiv of every segment
+    // the final launch's fresh instances (RicWork::tail): 1/kRicTailDiv of every segment when its retries start over
+    // (no memory for their iterates, or more hand-offs than the memory holds).  Resumed retries are short -- three
+    // trips on average instead of nine, eleven instead of twenty-one at most -- and fresh instances beside them only
+    // add their own stragglers: 27.15M QP/s without, 27.13M with 1/128, 26.8M with 1/32 on the 131,072-instance shard.
 #ifdef CARMPC_RIC_TAIL_ENV   // experiment builds only: divisor from the environment
     static const int tail_div = [] {
         const char* v = getenv("CARMPC_RIC_TAIL_DIV");
@@ -113,7 +165,8 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
 #else
     constexpr int tail_div = kRicTailDiv;
 #endif
-    for (int j = 0; j < T.nseg; ++j) W.tail[j] = tail_div > 0 ? (int32_t)((T.off[j + 1] - T.off[j]) / tail_div) : 0;
+    const bool fill = tail_div > 0 && W.state_cap < (int64_t)n;
+    for (int j = 0; j < T.nseg; ++j) W.tail[j] = fill ? (int32_t)((T.off[j + 1] - T.off[j]) / tail_div) : 0;
     // rounds of (iterations, polish): round r takes the instances whose first r polishes were rejected
     // (two or three per cent after round 0); what is left after the last round goes to the single kernel
     for (W.round = 0; W.round < kRicRounds && e == hipSuccess; ++W.round) {
@@ -121,7 +174,11 @@ hipError_t ric_pipeline(const RicSegs& T, int64_t total, const double* x0, const
         if (e == hipSuccess) e = ric_dispatch<false, 2>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
     }
     if (e == hipSuccess) e = ric_dispatch<false, 0>(T, W, total, x0, xref, u_out, ld_u, status, iters, s, stream, unsupported);
-    const hipError_t ef = hipFreeAsync(base, stream);
+    hipError_t ef = hipFreeAsync(base, stream);
+    if (state) {
+        const hipError_t es = hipFreeAsync(state, stream);
+        if (ef == hipSuccess) ef = es;
+    }
     return e != hipSuccess ? e : ef;
 }
 // Callers with their own instance list (closed loops: live slots, few per step) or claim counter (the

@@ -1203,7 +1203,10 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
     // slot -> row: the caller's list, the hand-off record (polish launch), or the slot itself
     auto row_of = [&](int64_t sl, bool lv) -> int64_t {
         if constexpr (MODE == 2) return lv ? (int64_t)(int32_t)W.pend_rec[(lst0 + sl) * kRicRecWords + kRicRecRow] : sl;
-        else if (MODE == 0 && W.cnt) return !lv ? sl : sl < nretry ? (int64_t)S.index[sl] : batch - ntail + (sl - nretry);
+        else if (MODE == 0 && W.cnt)   // a retry (its entry names the hand-off record, which holds the row) or a fresh instance of the tail
+            return !lv ? sl
+                   : sl < nretry ? (int64_t)(int32_t)W.pend_rec[(lst0 + S.index[sl]) * kRicRecWords + kRicRecRow]
+                                 : batch - ntail + (sl - nretry);
         else return lv && S.index ? (int64_t)S.index[sl] : sl;
     };
     int64_t inst = row_of(slot, live);
@@ -1383,6 +1386,35 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                 }
                 bnorm = 1.0 + row_max(bn);
                 qnorm = 1.0 + row_max(qn);
+                if constexpr (MODE == 0 && !HET) {
+                    // A retry whose iterate the iteration launch saved resumes from it: the same point from which the
+                    // single kernel carries on after a rejected polish (the trip below passes that polish over).
+                    if (W.cnt && slot < nretry) {
+                        const int64_t h = lst0 + S.index[slot];
+                        if (h < W.state_cap) {
+                            const double* st = W.state + h * kRicStateDoubles + j;
+#pragma unroll
+                            for (int s = 0; s < SL; ++s) {
+                                s_[s] = st[s * GL];
+                                z_[s] = st[(SL + s) * GL];
+                            }
+#pragma unroll
+                            for (int sg = 0; sg < NSG; ++sg) {
+#pragma unroll
+                                for (int a = 0; a < 4; ++a) xs[sg][a] = st[(2 * SL + sg * 14 + a) * GL];
+#pragma unroll
+                                for (int c = 0; c < 2; ++c) {
+                                    BX(F_U, sg, c) = st[(2 * SL + sg * 14 + 4 + c) * GL];
+                                    BX(F_SU, sg, c) = st[(2 * SL + sg * 14 + 6 + c) * GL];
+                                    BX(F_SL, sg, c) = st[(2 * SL + sg * 14 + 8 + c) * GL];
+                                    BX(F_ZU, sg, c) = st[(2 * SL + sg * 14 + 10 + c) * GL];
+                                    BX(F_ZL, sg, c) = st[(2 * SL + sg * 14 + 12 + c) * GL];
+                                }
+                            }
+                            it = (int)W.pend_rec[h * kRicRecWords + kRicRecIt];
+                        }
+                    }
+                }
             }
         }
         if constexpr (HET && !HL) {
@@ -1627,6 +1659,30 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         if (j == 0) {
                             hrec[kRicRecRow] = (uint32_t)inst;
                             hrec[kRicRecIt] = (uint32_t)it;
+                        }
+                        // the iterate itself, for the final launch should the polish be rejected (RicWork::state):
+                        // [quantity][lane of the group], every lane its own slots and inputs
+                        if ((int64_t)(lst0 + pos) < W.state_cap) {
+                            static_assert((2 * SL + 14 * NSG) * GL <= kRicStateDoubles, "state record");
+                            double* st = W.state + (int64_t)(lst0 + pos) * kRicStateDoubles + j;
+#pragma unroll
+                            for (int s = 0; s < SL; ++s) {
+                                st[s * GL] = s_[s];
+                                st[(SL + s) * GL] = z_[s];
+                            }
+#pragma unroll
+                            for (int sg = 0; sg < NSG; ++sg) {
+#pragma unroll
+                                for (int a = 0; a < 4; ++a) st[(2 * SL + sg * 14 + a) * GL] = xs[sg][a];
+#pragma unroll
+                                for (int c = 0; c < 2; ++c) {
+                                    st[(2 * SL + sg * 14 + 4 + c) * GL] = BX(F_U, sg, c);
+                                    st[(2 * SL + sg * 14 + 6 + c) * GL] = BX(F_SU, sg, c);
+                                    st[(2 * SL + sg * 14 + 8 + c) * GL] = BX(F_SL, sg, c);
+                                    st[(2 * SL + sg * 14 + 10 + c) * GL] = BX(F_ZU, sg, c);
+                                    st[(2 * SL + sg * 14 + 12 + c) * GL] = BX(F_ZL, sg, c);
+                                }
+                            }
                         }
                         finish(0, false, false);
                         active = false;
