@@ -98,3 +98,31 @@ def test_short_horizon_layouts_agree(gpu_available):
         assert same >= 0.999 and int((i1 - i0).abs().max()) <= 2, (chunk, same)
         ok = (s0 == 0)
         assert float((u1[ok] - u0[ok]).abs().max()) <= 1e-9, chunk
+
+
+def test_call_larger_than_the_saved_iterates(gpu_available):
+    """The iteration launch saves the iterate of every hand-off so that a rejected polish resumes from it, in
+    memory bounded per call (carmpc_internal.h: kRicStateMaxBytes, 279,620 instances).  A call beyond that
+    bound mixes the three kinds of work in its final launch -- resumed retries, retries that start over, and
+    the fresh instances it takes from the end of the batch when some retries start over -- and must return
+    what calls below the bound return (every retry resumed, no fresh instances): statuses, iteration counts
+    and u bit for bit, since every path runs the same arithmetic per instance."""
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build("RoadEnv", 20, terminal_set_dir=TERMINAL_SETS)     # (mostly feasible: more hand-offs than the bound holds)
+    qp = QPProblem(N=20, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    B, part = 393216, 131072
+    x = _x0(np.random.default_rng(23), asm.goal[0], B)
+    X = torch.as_tensor(x).to(qp.device)
+    u1, st1, it1 = qp.solve(X)
+    torch.cuda.synchronize()
+    assert int((st1 == 0).sum()) > 300000
+    for k in range(0, B, part):
+        u0, st0, it0 = qp.solve(X[k:k + part])
+        torch.cuda.synchronize()
+        bad = ((st0 != st1[k:k + part]) | (it0 != it1[k:k + part])).nonzero().flatten()
+        assert bad.numel() == 0, (k, bad[:8].tolist(), st0[bad[:8]].tolist(), st1[k:k + part][bad[:8]].tolist())
+        assert torch.equal(u0, u1[k:k + part])
