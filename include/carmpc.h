@@ -142,8 +142,11 @@ int carmpc_problem_get(const carmpc_problem* prob, double* T, double* S, double*
  * Stream-ordered on `stream`.  Device memory beyond the arguments comes from the stream-ordered
  * allocator: a claim counter, and for large batches of the grouped kernel (which then runs as
  * an iteration launch, a polish launch and a launch for the instances whose polish was rejected)
- * the work lists between those launches, 132 bytes per instance.  Results do not depend on which
- * form ran. */
+ * the work memory between those launches: 132 bytes per instance of lists, and 7,680 bytes per
+ * instance (at most 2 GiB per call) for the iterates from which rejected instances resume.  That
+ * memory comes from a pool of the library's own per device, which keeps it between calls and until
+ * the process ends (up to that much per call in flight).  Results do not depend on which form
+ * ran.  carmpc_solve_batch_noalloc below never takes any of it. */
 int carmpc_solve_batch(const carmpc_problem* prob, int64_t batch, const double* x0, const double* xref,
                        double* u_out, int32_t* status, int32_t* iters,
                        const carmpc_settings* settings, hipStream_t stream);
