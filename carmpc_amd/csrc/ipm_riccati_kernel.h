@@ -1502,6 +1502,11 @@ __global__ void __launch_bounds__(WPB * 64) ipm_riccati_kernel(RicSegs T, RicWor
                         add_qbar(kseg[sg] == N, xs[sg], h, 1.0);
                         wr4((kseg[sg] - 1) * REC + 0, v);
                         wr4((kseg[sg] - 1) * REC + 4, h);
+                        // The passes' source of structural zeros, rewritten with the record's other inputs: the passes
+                        // run for the whole wave, and while a group sits one out on records that hold non-finite
+                        // leftovers (the pair check's NaN marks, an overflow on stale data), its lanes store 0 x that
+                        // = NaN into this slot.
+                        if constexpr (!HL) rec[(kseg[sg] - 1) * REC + O_ZERO] = 0.0;
                     }
                 RT_MARK(1);
                 mu = row_sum(musum) * inv_m;
