@@ -270,6 +270,16 @@ class GpuBackend:
             sh.copy_(self.st, non_blocking=True)
         torch.cuda.synchronize()
         self.e2e_serial = 3 * X.shape[0] / (time.perf_counter() - t0)
+        # the first input of every sequence back to the host (what the reference's step() returns), one batch at a time
+        hp1 = HostPipeline(self.probs, self.offsets, settings=self.settings, depth=1, first_action=True)
+        hp1.staging(0).copy_(Xt)
+        u_first = hp1.wait(hp1.submit())[0]
+        self.e2e_first_ok = bool(np.array_equal(u_first.numpy(), self.u[:, :u_first.shape[1]].cpu().numpy()))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(6):
+            hp1.wait(hp1.submit())
+        self.e2e_first = 6 * X.shape[0] / (time.perf_counter() - t0)
         return stream_rate
 
 
@@ -421,6 +431,9 @@ def run(args, backend_cls=None) -> dict | None:
             out["e2e_qps_pcie_one_batch_at_a_time"] = round(be.e2e_single * world, 1)
         if getattr(be, "e2e_serial", None):
             out["e2e_qps_pcie_serial_one_stream"] = round(be.e2e_serial * world, 1)
+        if getattr(be, "e2e_first", None):
+            out["e2e_qps_pcie_first_action_only"] = round(be.e2e_first * world, 1)
+            out["e2e_first_action_equals_resident"] = be.e2e_first_ok
         chk = getattr(be, "e2e_check", None)
         if chk is not None:       # the chunked path returns the same statuses and iteration counts
             out["e2e_equals_resident"] = bool(np.array_equal(chk[0], st_np) and np.array_equal(chk[1], it_np))

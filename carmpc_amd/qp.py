@@ -458,12 +458,19 @@ class HostPipeline:
     the solve alone.  ``solve`` is submit + wait for one batch.  Results are those of one ``solve_segments``
     call on resident data.
 
+    ``first_action`` returns what the reference's ``step`` returns -- the first input of every optimal sequence
+    (mpc.py:349: ``u.value[:nu]``; the rest of the horizon is kept there for plots only) -- so the copy back to
+    the host is nu instead of N nu doubles per instance: 2 MB instead of 42 MB for 131,072 instances at N = 20,
+    and the host-memory rate is within a few per cent of the resident one.
+
     ``chunks`` (row counts) cuts one batch into several solve calls whose copies overlap inside the batch;
     measured on the 131,072-instance mixed shard this is slower than one call (every call ends with its own
-    latency-bound launch tails: 7.1 ms unchunked, 7.7-8.4 ms for two to four chunks), so the default is one.
-    Batches in flight, same shard: one 18.6M QP/s, two 16.7M, three 19.7M (resident data: 21.6M)."""
+    latency-bound launch tails), so the default is one.  Batches in flight, same shard, full sequences back:
+    one 22M QP/s, two 19-21M, three 18-24M (resident data: 27M) -- a copy that runs beside a solve slows the
+    solve by about what it saves."""
 
-    def __init__(self, problems: list, offsets, chunks=None, settings: SolverSettings | None = None, depth: int = 3):
+    def __init__(self, problems: list, offsets, chunks=None, settings: SolverSettings | None = None, depth: int = 3,
+                 first_action: bool = False):
         self.problems = list(problems)
         self.dev = problems[0].device
         self.offsets = [int(o) for o in offsets]
@@ -471,6 +478,13 @@ class HostPipeline:
             raise ValueError("offsets must start at 0 and have len(problems) + 1 entries")
         self.B = B = self.offsets[-1]
         self.ld = max(p.n for p in problems)
+        #: columns of u copied back to the host: the whole sequence, or the first input (nu entries) of each
+        self.ncopy = self.ld
+        if first_action:
+            nus = {p.nu for p in problems}
+            if len(nus) != 1 or None in nus:
+                raise ValueError("first_action needs stage-structured problems with one input dimension")
+            self.ncopy = int(nus.pop())
         self.settings = settings or SolverSettings()
         chunks = [B] if chunks is None else [int(c) for c in chunks if int(c) > 0]
         if sum(chunks) != B:
@@ -487,7 +501,7 @@ class HostPipeline:
                          st=torch.empty(B, dtype=torch.int32, device=self.dev),
                          it=torch.empty(B, dtype=torch.int32, device=self.dev))
             d.update(Xh=torch.empty((B, NX), dtype=torch.float64).pin_memory(),
-                     uh=torch.empty((B, self.ld), dtype=torch.float64).pin_memory(),
+                     uh=torch.empty((B, self.ncopy), dtype=torch.float64).pin_memory(),
                      sth=torch.empty(B, dtype=torch.int32).pin_memory(),
                      ith=torch.empty(B, dtype=torch.int32).pin_memory(), done=None)
             self.sets.append(d)
@@ -532,7 +546,7 @@ class HostPipeline:
                 ev_done.record(self.s_solve)
                 self.s_out.wait_event(ev_done)
                 with torch.cuda.stream(self.s_out):
-                    d["uh"][r0:r1].copy_(d["u"][r0:r1], non_blocking=True)
+                    d["uh"][r0:r1].copy_(d["u"][r0:r1, :self.ncopy], non_blocking=True)
                     d["sth"][r0:r1].copy_(d["st"][r0:r1], non_blocking=True)
                     d["ith"][r0:r1].copy_(d["it"][r0:r1], non_blocking=True)
             with torch.cuda.stream(self.s_out):

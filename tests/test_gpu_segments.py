@@ -173,6 +173,12 @@ def test_host_pipeline_equals_resident_solve(gpu_available):
             np.testing.assert_array_equal(st.numpy(), s0)
             np.testing.assert_array_equal(it.numpy(), i0)
             np.testing.assert_allclose(u.numpy()[ok], u0[ok], rtol=0, atol=1e-12)
+    # only the first input of every sequence back to the host (what the reference's step() returns, mpc.py:349)
+    hp = HostPipeline(probs, offsets, depth=1, first_action=True)
+    u, st, it = hp.solve(X)
+    assert u.shape == (B, 2)
+    np.testing.assert_array_equal(st.numpy(), s0)
+    np.testing.assert_allclose(u.numpy()[ok], u0[ok][:, :2], rtol=0, atol=1e-12)
     # a sequence of batches with two in flight: batch k's results are those of batch k's states
     hp = HostPipeline(probs, offsets, depth=2)
     Xs = [X, X[::-1].copy(), X]                 # (the reversed batch puts other states under each problem)
