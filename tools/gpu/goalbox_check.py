@@ -13,13 +13,14 @@ from oracle.cpu import CpuProblem  # noqa: E402
 from carmpc_amd.qp import QPProblem, SolverSettings  # noqa: E402
 
 tmp = tempfile.mkdtemp()
-for N in (5, 10):
+for N in (5, 10, 20):
     asm = oa.build("RoadEnv", N, terminal_set_dir=tmp)
     qp = QPProblem(N=N, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
                    state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
                    term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
     rng = np.random.default_rng(N)
-    X = np.stack([rng.uniform(28, 30, 200), rng.uniform(1, 2, 200), rng.uniform(-0.05, 0.05, 200), rng.uniform(-0.2, 0.2, 200)], axis=1)
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    X = np.stack([rng.uniform(30 - 0.2 * N, 30, B), rng.uniform(1, 2, B), rng.uniform(-0.05, 0.05, B), rng.uniform(-0.2, 0.2, B)], axis=1)
     uc, sc, ic = CpuProblem(asm).solve(X)
     Xd = torch.as_tensor(X).cuda()
     for rep in range(6):
