@@ -126,3 +126,30 @@ def test_call_larger_than_the_saved_iterates(gpu_available):
         bad = ((st0 != st1[k:k + part]) | (it0 != it1[k:k + part])).nonzero().flatten()
         assert bad.numel() == 0, (k, bad[:8].tolist(), st0[bad[:8]].tolist(), st1[k:k + part][bad[:8]].tolist())
         assert torch.equal(u0, u1[k:k + part])
+
+
+def test_work_memory_is_reused_between_calls(gpu_available):
+    """The pipeline's work memory (lists and saved iterates, about 1 GB for 131,072 instances) comes from a
+    stream-ordered pool that keeps it between calls: after a warm call, synchronised calls of the same size leave
+    the free device memory where it was (no growth per call, no allocation and release per call)."""
+    import torch
+    from oracle import assembly as oa
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build("RoadOneCarEnv", 20, terminal_set_dir=TERMINAL_SETS)
+    qp = QPProblem(N=20, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    B = 131072
+    X = torch.as_tensor(_x0(np.random.default_rng(3), asm.goal[0], B)).to(qp.device)
+    out = (torch.empty((B, qp.n), dtype=torch.float64, device=qp.device),
+           torch.empty(B, dtype=torch.int32, device=qp.device), torch.empty(B, dtype=torch.int32, device=qp.device))
+    for _ in range(2):
+        qp.solve(X, out=out)
+        torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    st0 = out[1].clone()
+    for _ in range(10):
+        qp.solve(X, out=out)
+        torch.cuda.synchronize()
+        assert torch.cuda.mem_get_info()[0] == free0
+    assert torch.equal(out[1], st0)
