@@ -550,7 +550,7 @@ int stage_observer(const carmpc_problem* P, int32_t ny, const double* C, const d
 extern "C" {
 
 const char* carmpc_last_error(void) { return g_err.c_str(); }
-const char* carmpc_version(void) { return "carmpc-mi355x 0.5 (gfx950: riccati launch pipeline / staged / dense IPM, closed loop, batched LP, per-instance linearisation, CPU path)"; }
+const char* carmpc_version(void) { return "carmpc-mi355x 0.6 (gfx950: riccati launch pipeline / staged / dense IPM, closed loop, batched LP, per-instance linearisation, CPU path)"; }
 
 int carmpc_problem_kernel(const carmpc_problem* P) {
     if (!P) return fail(CARMPC_EINVAL, "null problem");

@@ -340,7 +340,7 @@ struct MtH {
 // the issue slots the first leaves idle while it waits for its own dependent results.  The matrix-core passes
 // then carry two QPs in blocks 0 and 1; blocks 2 and 3 repeat them (same loads, same values stored).
 //
-// SEGS = slot segments per lane.  With 16 lanes per QP the default is two (the round-2 layout, 16 row slots per
+// SEGS = slot segments per lane.  With 16 lanes per QP the default is two (the original layout, 16 row slots per
 // lane); SEGS = 1 with 16 lanes is the layout for short horizons whose rows fit the first segment alone (N <= 16,
 // capi.hip::riccati_layout, DevProblem::rone): FOUR QPs per wavefront at the per-lane state of the 32-lane
 // layout, so eight waves of four QPs share a CU -- twice the QPs per instruction.
