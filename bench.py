@@ -487,8 +487,8 @@ def run(args, backend_cls=None) -> dict | None:
         out["roofline"] = {
             "bound": "mfma",
             "compute": "FP64: v_mfma_f64_4x4x4 (stage recursions) and vector FMA (row phases); both pipes peak at "
-                       "78.6 TFLOP/s.  The measured limiter is LDS / issue latency at one wavefront per SIMD, not "
-                       "either pipe's rate",
+                       "78.6 TFLOP/s.  The measured limiter is instruction issue at two wavefronts per SIMD (about one "
+                       "instruction per 4 cycles and SIMD), not either pipe's arithmetic rate",
             "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
             "frac_is": "canonical dense-IPM flops (p n^2 + n^3/3 + 6 n^2 + 12 p n per iteration) x the oracle's "
@@ -500,7 +500,11 @@ def run(args, backend_cls=None) -> dict | None:
             "issued_frac": round(issued_tf / FP64_PEAK_TFLOPS, 5),
             "issued_is": "as executed_frac, with every matrix-core instruction counted as a full 4x4x4 product "
                          "(part of the operands are structural zeros or replicated columns): FP64 pipe occupancy",
-            "traffic": traffic, "algorithmic_bytes_per_step": B * per_qp,
+            "traffic": traffic,
+            "traffic_is": "HBM bytes per step from the FETCH_SIZE / WRITE_SIZE counters of the committed profile "
+                          "(profiles/traffic.json); about 0.79 GB of it are the iterates the iteration launch saves "
+                          "with every hand-off (written once; read back for the few per cent whose polish is rejected)",
+            "algorithmic_bytes_per_step": B * per_qp,
             "algorithmic_hbm_GBps": round(B * per_qp / (kern_ms * 1e-3) / 1e9, 3),
             "hbm_frac": round(B * per_qp / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6),
             "kernel_ms_per_step": round(kern_ms, 4), "canonical_flops_per_step": flops_step,
