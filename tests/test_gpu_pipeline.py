@@ -153,3 +153,36 @@ def test_work_memory_is_reused_between_calls(gpu_available):
         torch.cuda.synchronize()
         assert torch.cuda.mem_get_info()[0] == free0
     assert torch.equal(out[1], st0)
+
+
+@pytest.mark.parametrize("N", [10, 20])
+def test_paired_rows_through_the_pipeline(gpu_available, tmp_path, N):
+    """Problems whose terminal set is the goal box (missing terminal-set file, mpc.py:107-117: opposite rows
+    paired into equalities, which the polish acceptance test handles through a shared scratch buffer) at a
+    batch size that runs as three launches -- with four QPs per wavefront at N = 10 and two at N = 20:
+    statuses and iteration counts of every instance against the C oracle."""
+    import torch
+    from oracle import assembly as oa
+    from oracle.cpu import CpuProblem
+    from carmpc_amd.qp import QPProblem
+    asm = oa.build("RoadEnv", N, terminal_set_dir=str(tmp_path))
+    assert asm.term_file is None
+    qp = QPProblem(N=N, A=asm.A, B=asm.B, Q=oa.STAGE_COST_Q, R=oa.STAGE_COST_R, P=asm.P, goal=asm.goal,
+                   state_A=np.asarray(asm.state_rows_A, float), state_b=np.asarray(asm.state_rows_b, float),
+                   term_A=asm.term_A[:, -4:], term_b=asm.term_b, u_lower=asm.input_lower, u_upper=asm.input_upper)
+    assert qp.kernel == 7
+    B = 65536
+    rng = np.random.default_rng(100 + N)
+    X = np.stack([rng.uniform(30 - 0.2 * N, 30, B), rng.uniform(1, 2, B), rng.uniform(-0.05, 0.05, B),
+                  rng.uniform(-0.2, 0.2, B)], axis=1)
+    uc, sc, ic = CpuProblem(asm).solve(X)
+    assert int((sc == 0).sum()) > B // 4
+    Xd = torch.as_tensor(X).cuda()
+    for _ in range(3):
+        u, st, it = qp.solve(Xd)
+        torch.cuda.synchronize()
+        st, it = st.cpu().numpy(), it.cpu().numpy()
+        np.testing.assert_array_equal(st, sc)
+        ok = sc == 0
+        np.testing.assert_array_equal(it[ok], ic[ok])
+        assert np.abs(u.cpu().numpy()[ok] - uc[ok]).max() <= 1e-6
